@@ -1,0 +1,659 @@
+// capi.cpp -- the extern "C" boundary of include/atray.h: scene flattening + upload, render
+// launches on a HIP stream, progress/wait, and the host prerequisites behind opaque handles.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine.h"
+#include "host_scene.h"
+
+using namespace atr;
+
+extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s);
+extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
+                                        const uint32_t* packed, uint32_t* image, hipStream_t s);
+extern "C" hipError_t atr_launch_tile_casts(const atr_tile* tiles, int32_t ntiles, int32_t width,
+                                            const uint32_t* casts, int64_t* out, hipStream_t s);
+
+#define HIPCHK(x)                                      \
+    do {                                               \
+        hipError_t e_ = (x);                           \
+        if (e_ != hipSuccess) return -(1000 + int(e_)); \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+// Blocks for one tile list: the 8x8 cells covering the union of the (inclusive) tile rects,
+// each pixel owned exactly once (the reference traces the 1-px overlaps twice, renderer.cpp:429-442).
+struct BlockSet {
+    std::vector<atr_tile> tiles;
+    int32_t width = 0, height = 0;
+    std::vector<DBlock> host;
+    DevBuf dev;
+    DevBuf dev_tiles;
+    int64_t packed_pixels = 0;
+};
+
+void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, std::vector<DBlock>& out,
+                  int64_t& npix) {
+    const int32_t cw = (W + 7) / 8, ch = (H + 7) / 8;
+    std::vector<uint64_t> cell(size_t(cw) * size_t(ch), 0);
+    // tile order decides the block order: cells are emitted tile by tile (first owner wins)
+    std::vector<int32_t> order;
+    order.reserve(cell.size());
+    std::vector<uint8_t> seen(cell.size(), 0);
+    for (int32_t k = 0; k < ntiles; ++k) {
+        atr_tile t = tiles[k];
+        if (t.min_x < 0) t.min_x = 0;
+        if (t.min_y < 0) t.min_y = 0;
+        if (t.max_x > W - 1) t.max_x = W - 1;
+        if (t.max_y > H - 1) t.max_y = H - 1;
+        if (t.max_x < t.min_x || t.max_y < t.min_y) continue;
+        for (int32_t cy = t.min_y / 8; cy <= t.max_y / 8; ++cy)
+            for (int32_t cx = t.min_x / 8; cx <= t.max_x / 8; ++cx) {
+                const size_t ci = size_t(cy) * size_t(cw) + size_t(cx);
+                uint64_t m = 0;
+                for (int32_t ly = 0; ly < 8; ++ly) {
+                    const int32_t y = cy * 8 + ly;
+                    if (y < t.min_y || y > t.max_y) continue;
+                    for (int32_t lx = 0; lx < 8; ++lx) {
+                        const int32_t x = cx * 8 + lx;
+                        if (x >= t.min_x && x <= t.max_x) m |= uint64_t(1) << (ly * 8 + lx);
+                    }
+                }
+                if (!m) continue;
+                if (!seen[ci]) { seen[ci] = 1; order.push_back(int32_t(ci)); }
+                cell[ci] |= m;
+            }
+    }
+    out.clear();
+    out.reserve(order.size());
+    npix = 0;
+    for (int32_t ci : order) {
+        DBlock b;
+        std::memset(&b, 0, sizeof(b));
+        b.x0 = (ci % cw) * 8;
+        b.y0 = (ci / cw) * 8;
+        b.mask_lo = uint32_t(cell[size_t(ci)]);
+        b.mask_hi = uint32_t(cell[size_t(ci)] >> 32);
+        b.out_base = int32_t(npix);
+        npix += __builtin_popcountll(cell[size_t(ci)]);
+        out.push_back(b);
+    }
+}
+
+}  // namespace
+
+struct atr_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr, ev_done = nullptr;
+    bool have_render = false;
+    int32_t last_ntiles = 0;
+    std::vector<DevBuf> scene_bufs;
+    DScene* d_scene = nullptr;
+    int64_t scene_bytes = 0;
+    int32_t max_nodes = 0, max_depth = 0, nmodels = 0;
+    static constexpr int kBlockSlots = 24;  // tile-list cache: own render + one unpack per rank
+    BlockSet blocks[kBlockSlots];
+    uint64_t block_use[kBlockSlots] = {};
+    uint64_t use_clock = 0;
+    int32_t* d_error = nullptr;
+};
+
+namespace {
+
+int dev_upload(atr_ctx* c, const void* src, size_t bytes, void** out) {
+    DevBuf b;
+    b.n = bytes ? bytes : 16;
+    HIPCHK(hipMalloc(&b.p, b.n));
+    if (bytes) HIPCHK(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    c->scene_bufs.push_back(b);
+    c->scene_bytes += int64_t(b.n);
+    *out = b.p;
+    return ATR_OK;
+}
+
+void free_scene(atr_ctx* c) {
+    for (DevBuf& b : c->scene_bufs) (void)hipFree(b.p);
+    c->scene_bufs.clear();
+    c->d_scene = nullptr;
+    c->scene_bytes = 0;
+}
+
+BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, int& rc) {
+    rc = ATR_OK;
+    int lru = 0;
+    for (int i = 0; i < atr_ctx::kBlockSlots; ++i) {
+        BlockSet& b = c->blocks[i];
+        if (b.width == W && b.height == H && int32_t(b.tiles.size()) == ntiles && b.dev.p &&
+            (ntiles == 0 || std::memcmp(b.tiles.data(), tiles, sizeof(atr_tile) * size_t(ntiles)) == 0)) {
+            c->block_use[i] = ++c->use_clock;
+            return &b;
+        }
+        if (c->block_use[i] < c->block_use[lru]) lru = i;
+    }
+    BlockSet& b = c->blocks[lru];
+    c->block_use[lru] = ++c->use_clock;
+    // the slot may still be read by an in-flight kernel of an earlier render
+    if (c->have_render) (void)hipEventSynchronize(c->ev_done);
+    b.tiles.assign(tiles, tiles + ntiles);
+    b.width = W;
+    b.height = H;
+    build_blocks(tiles, ntiles, W, H, b.host, b.packed_pixels);
+    const size_t need = std::max<size_t>(b.host.size() * sizeof(DBlock), 32);
+    if (b.dev.n < need) {
+        if (b.dev.p) (void)hipFree(b.dev.p);
+        b.dev = DevBuf();
+        if (hipMalloc(&b.dev.p, need) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
+        b.dev.n = need;
+    }
+    const size_t tneed = std::max<size_t>(sizeof(atr_tile) * size_t(ntiles), 16);
+    if (b.dev_tiles.n < tneed) {
+        if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
+        b.dev_tiles = DevBuf();
+        if (hipMalloc(&b.dev_tiles.p, tneed) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
+        b.dev_tiles.n = tneed;
+    }
+    hipError_t e = hipMemcpy(b.dev.p, b.host.data(), b.host.size() * sizeof(DBlock), hipMemcpyHostToDevice);
+    if (e == hipSuccess && ntiles)
+        e = hipMemcpy(b.dev_tiles.p, tiles, sizeof(atr_tile) * size_t(ntiles), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { rc = -(1000 + int(e)); b.width = -1; return nullptr; }
+    return &b;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* atr_version(void) { return "atray-mi355x 0.1 (gfx950)"; }
+
+// ------------------------------------------------------------------ host prerequisites
+int atr_mesh_parse_obj(const char* text, size_t len, atr_mesh** out) {
+    if (!text || !out) return ATR_E_INVALID;
+    atr_mesh* m = new (std::nothrow) atr_mesh();
+    if (!m) return ATR_E_NOMEM;
+    const int rc = parse_obj_text(text, len, m->m);
+    if (rc != ATR_OK) { delete m; return rc; }
+    *out = m;
+    return ATR_OK;
+}
+
+int atr_mesh_load_obj(const char* path, atr_mesh** out) {
+    if (!path || !out) return ATR_E_INVALID;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return ATR_E_IO;
+    std::string buf;
+    char tmp[1 << 16];
+    size_t n;
+    while ((n = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.append(tmp, n);
+    std::fclose(f);
+    return atr_mesh_parse_obj(buf.data(), buf.size(), out);
+}
+
+int atr_mesh_from_arrays(const float* vertices, uint32_t nvertices, const int32_t* face_vertices,
+                         uint32_t nfaces, const float* normals, uint32_t nnormals,
+                         const int32_t* face_normals, atr_mesh** out) {
+    if (!out || (nvertices && !vertices) || (nfaces && !face_vertices)) return ATR_E_INVALID;
+    if (nnormals && (!normals || !face_normals)) return ATR_E_INVALID;
+    atr_mesh* m = new (std::nothrow) atr_mesh();
+    if (!m) return ATR_E_NOMEM;
+    for (uint32_t i = 0; i < nvertices; ++i) m->m.vertices.push_back(mk(vertices[3 * i], vertices[3 * i + 1], vertices[3 * i + 2]));
+    for (uint32_t i = 0; i < nnormals; ++i) m->m.normals.push_back(mk(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]));
+    m->m.face_v.assign(face_vertices, face_vertices + 3 * size_t(nfaces));
+    m->m.face_t.assign(3 * size_t(nfaces), -1);
+    if (nnormals) m->m.face_n.assign(face_normals, face_normals + 3 * size_t(nfaces));
+    else m->m.face_n.assign(3 * size_t(nfaces), -1);
+    *out = m;
+    return ATR_OK;
+}
+
+void atr_mesh_free(atr_mesh* m) { delete m; }
+
+int atr_mesh_info(const atr_mesh* m, uint32_t* nv, uint32_t* nn, uint32_t* nf) {
+    if (!m) return ATR_E_INVALID;
+    if (nv) *nv = uint32_t(m->m.vertices.size());
+    if (nn) *nn = uint32_t(m->m.normals.size());
+    if (nf) *nf = uint32_t(m->m.nfaces());
+    return ATR_OK;
+}
+
+int atr_mesh_aabb(const atr_mesh* m, float aabb_out[6]) {
+    if (!m || !aabb_out) return ATR_E_INVALID;
+    mesh_aabb(m->m, aabb_out);
+    return ATR_OK;
+}
+
+int atr_mesh_translate_to(atr_mesh* m, float aabb[6], atr_vec3 c) {
+    if (!m || !aabb) return ATR_E_INVALID;
+    mesh_translate(m->m, aabb, mk(c.x, c.y, c.z));
+    return ATR_OK;
+}
+
+int atr_octree_build(const atr_mesh* m, uint32_t max_faces, atr_octree** out) {
+    if (!m || !out) return ATR_E_INVALID;
+    atr_octree* t = new (std::nothrow) atr_octree();
+    if (!t) return ATR_E_NOMEM;
+    const int rc = octree_build(m->m, max_faces, t->t);
+    if (rc != ATR_OK) { delete t; return rc; }
+    *out = t;
+    return ATR_OK;
+}
+
+int atr_octree_from_nodes(int32_t nnodes, const float* bounds, const int32_t* children,
+                          const uint32_t* leaf_first, const uint32_t* leaf_count, uint32_t nprims,
+                          const float* prim_vertices, const uint32_t* prim_face, atr_octree** out) {
+    if (nnodes <= 0 || !bounds || !children || !leaf_first || !leaf_count || !out) return ATR_E_INVALID;
+    if (nprims && (!prim_vertices || !prim_face)) return ATR_E_INVALID;
+    atr_octree* t = new (std::nothrow) atr_octree();
+    if (!t) return ATR_E_NOMEM;
+    HostTree& T = t->t;
+    T.nnodes = nnodes;
+    T.bounds.assign(bounds, bounds + 6 * size_t(nnodes));
+    T.children.assign(children, children + nnodes);
+    T.leaf_first.assign(leaf_first, leaf_first + nnodes);
+    T.leaf_count.assign(leaf_count, leaf_count + nnodes);
+    T.prim_vertices.assign(prim_vertices, prim_vertices + 9 * size_t(nprims));
+    T.prim_face.assign(prim_face, prim_face + nprims);
+    for (int32_t i = 0; i < nnodes; ++i)
+        if (children[i] == 0 && uint64_t(leaf_first[i]) + leaf_count[i] > nprims) { delete t; return ATR_E_INVALID; }
+    const int rc = octree_finish(T);
+    if (rc != ATR_OK) { delete t; return rc; }
+    *out = t;
+    return ATR_OK;
+}
+
+void atr_octree_free(atr_octree* t) { delete t; }
+
+int atr_octree_export(const atr_octree* t, float* bounds, int32_t* children, uint32_t* leaf_first,
+                      uint32_t* leaf_count, float* prim_vertices, uint32_t* prim_face) {
+    if (!t) return ATR_E_INVALID;
+    const HostTree& T = t->t;
+    if (bounds) std::memcpy(bounds, T.bounds.data(), T.bounds.size() * sizeof(float));
+    if (children) std::memcpy(children, T.children.data(), T.children.size() * sizeof(int32_t));
+    if (leaf_first) std::memcpy(leaf_first, T.leaf_first.data(), T.leaf_first.size() * sizeof(uint32_t));
+    if (leaf_count) std::memcpy(leaf_count, T.leaf_count.data(), T.leaf_count.size() * sizeof(uint32_t));
+    if (prim_vertices) std::memcpy(prim_vertices, T.prim_vertices.data(), T.prim_vertices.size() * sizeof(float));
+    if (prim_face) std::memcpy(prim_face, T.prim_face.data(), T.prim_face.size() * sizeof(uint32_t));
+    return ATR_OK;
+}
+
+int atr_octree_stats(const atr_octree* t, int64_t s[7]) {
+    if (!t || !s) return ATR_E_INVALID;
+    octree_stats(t->t, s);
+    return ATR_OK;
+}
+
+int atr_camera_set(atr_camera* cm, atr_vec3 eye, atr_vec3 facing, int32_t w, int32_t h, int32_t aa,
+                   uint32_t spp, int32_t bounces, float h_fov) {
+    if (!cm || w <= 0 || h <= 0) return ATR_E_INVALID;
+    camera_set(*cm, mk(eye.x, eye.y, eye.z), mk(facing.x, facing.y, facing.z), w, h, aa, spp, bounces, h_fov);
+    return ATR_OK;
+}
+
+int32_t atr_make_tiles(int32_t w, int32_t h, int32_t threads, atr_tile* out, int32_t cap) {
+    return reference_tiles(w, h, threads, out, out ? cap : 0);
+}
+
+int32_t atr_make_shard_tiles(int32_t w, int32_t h, int32_t side, int32_t rank, int32_t world, atr_tile* out,
+                             int32_t cap) {
+    return shard_tiles(w, h, side, rank, world, out, out ? cap : 0);
+}
+
+// ------------------------------------------------------------------ device engine
+int atr_create(int device, atr_ctx** out) {
+    if (!out) return ATR_E_INVALID;
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(device));
+    atr_ctx* c = new (std::nothrow) atr_ctx();
+    if (!c) return ATR_E_NOMEM;
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev_start));
+    HIPCHK(hipEventCreate(&c->ev_stop));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&c->d_error, 16));
+    HIPCHK(hipMemset(c->d_error, 0, 16));
+    *out = c;
+    return ATR_OK;
+}
+
+int atr_destroy(atr_ctx* c) {
+    if (!c) return ATR_E_INVALID;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    free_scene(c);
+    for (BlockSet& b : c->blocks) {
+        if (b.dev.p) (void)hipFree(b.dev.p);
+        if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
+    }
+    if (c->d_error) (void)hipFree(c->d_error);
+    (void)hipEventDestroy(c->ev_start);
+    (void)hipEventDestroy(c->ev_stop);
+    (void)hipEventDestroy(c->ev_done);
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return ATR_OK;
+}
+
+int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const atr_model* models,
+                     int32_t nmodels, const atr_sphere* spheres, int32_t nspheres, const atr_plane* planes,
+                     int32_t nplanes) {
+    if (!c || !mats || nmats <= 0 || nmats > kMaxMaterials || nmodels < 0 || nmodels > kMaxModels ||
+        (nmodels && !models) || nspheres < 0 || nplanes < 0 || (nspheres && !spheres) || (nplanes && !planes))
+        return ATR_E_INVALID;
+    for (int32_t i = 0; i < nmodels; ++i) {
+        const atr_model& md = models[i];
+        if (!md.mesh || md.material < 0 || md.material >= nmats) return ATR_E_INVALID;
+        if (md.tree) {
+            for (int32_t d : md.tree->t.depth)
+                if (d >= kMaskLevels) return ATR_E_TREE_DEPTH;
+        }
+    }
+    HIPCHK(hipSetDevice(c->device));
+    if (c->have_render) HIPCHK(hipEventSynchronize(c->ev_done));
+    free_scene(c);
+    DScene S;
+    std::memset(&S, 0, sizeof(S));
+    for (int32_t i = 0; i < nmats; ++i) {
+        const atr_material& m = mats[i];
+        S.mats[i] = DMaterial{m.emission.x, m.emission.y, m.emission.z, m.reflection.x, m.reflection.y,
+                              m.reflection.z, m.scatter, 0.f};
+    }
+    S.nmats = nmats;
+    S.nmodels = nmodels;
+    c->max_nodes = 0;
+    c->max_depth = 0;
+    for (int32_t i = 0; i < nmodels; ++i) {
+        const atr_model& md = models[i];
+        const HostMesh& M = md.mesh->m;
+        DModel& dm = S.models[i];
+        std::memset(&dm, 0, sizeof(dm));
+        const size_t nf = M.nfaces();
+        dm.nfaces = uint32_t(nf);
+        dm.material = md.material;
+        std::memcpy(dm.aabb, md.surrounding_aabb, sizeof(dm.aabb));
+        dm.smooth = M.normals.empty() ? 0 : 1;
+        auto make_tri = [](const float* v, uint32_t face) {
+            DTri t;
+            std::memset(&t, 0, sizeof(t));
+            const V3 a = mk(v[0], v[1], v[2]), b = mk(v[3], v[4], v[5]), cc = mk(v[6], v[7], v[8]);
+            const V3 ab = sub(b, a), ac = sub(cc, a);  // model.h:77-78, once per primitive
+            t.ax = a.x; t.ay = a.y; t.az = a.z;
+            t.abx = ab.x; t.aby = ab.y; t.abz = ab.z;
+            t.acx = ac.x; t.acy = ac.y; t.acz = ac.z;
+            t.face = face;
+            return t;
+        };
+        // per-face shading record (renderer.cpp:124-149)
+        std::vector<float> shade(9 * (nf ? nf : 1), 0.f);
+        for (size_t f = 0; f < nf; ++f) {
+            for (int k = 0; k < 3; ++k) {
+                V3 v = mk(0.f, 0.f, 0.f);
+                if (dm.smooth) {
+                    const int32_t ni = M.face_n[3 * f + size_t(k)];
+                    if (ni >= 0 && size_t(ni) < M.normals.size()) v = M.normals[size_t(ni)];
+                } else {
+                    const int32_t vi = M.face_v[3 * f + size_t(k)];
+                    if (vi >= 0 && size_t(vi) < M.vertices.size()) v = M.vertices[size_t(vi)];
+                }
+                shade[9 * f + 3 * size_t(k)] = v.x;
+                shade[9 * f + 3 * size_t(k) + 1] = v.y;
+                shade[9 * f + 3 * size_t(k) + 2] = v.z;
+            }
+        }
+        void* p = nullptr;
+        int rc = dev_upload(c, shade.data(), shade.size() * sizeof(float), &p);
+        if (rc) return rc;
+        dm.shade = static_cast<const float*>(p);
+        if (md.tree) {
+            const HostTree& T = md.tree->t;
+            std::vector<DNode> nodes(size_t(T.nnodes));
+            std::vector<uint32_t> range(2 * size_t(T.nnodes), 0);
+            for (int32_t n = 0; n < T.nnodes; ++n) {
+                DNode& d = nodes[size_t(n)];
+                const float* b = &T.bounds[6 * size_t(n)];
+                d.lo_x = b[0]; d.lo_y = b[1]; d.lo_z = b[2];
+                d.hi_x = b[3]; d.hi_y = b[4]; d.hi_z = b[5];
+                d.children = T.children[size_t(n)];
+                d.parent = T.parent[size_t(n)];
+                range[2 * size_t(n)] = T.leaf_first[size_t(n)];
+                range[2 * size_t(n) + 1] = T.children[size_t(n)] ? 0u : T.leaf_count[size_t(n)];
+                if (T.depth[size_t(n)] > c->max_depth) c->max_depth = T.depth[size_t(n)];
+            }
+            std::vector<DTri> tris(T.prim_face.size());
+            for (size_t k = 0; k < tris.size(); ++k) tris[k] = make_tri(&T.prim_vertices[9 * k], T.prim_face[k]);
+            if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
+            dm.nodes = static_cast<const DNode*>(p);
+            if ((rc = dev_upload(c, range.data(), range.size() * sizeof(uint32_t), &p))) return rc;
+            dm.leaf_range = static_cast<const uint32_t*>(p);
+            if ((rc = dev_upload(c, tris.data(), tris.size() * sizeof(DTri), &p))) return rc;
+            dm.tris = static_cast<const DTri*>(p);
+            dm.has_tree = 1;
+            dm.root_leaf = T.children[0] == 0;
+            if (T.nnodes > c->max_nodes) c->max_nodes = T.nnodes;
+        } else {  // brute force: face-ordered triangles straight from the mesh (renderer.cpp:61-66)
+            std::vector<DTri> tris(nf);
+            for (size_t f = 0; f < nf; ++f) {
+                float v[9];
+                for (int k = 0; k < 3; ++k) {
+                    const int32_t vi = M.face_v[3 * f + size_t(k)];
+                    if (vi < 0 || size_t(vi) >= M.vertices.size()) return ATR_E_INVALID;
+                    const V3 q = M.vertices[size_t(vi)];
+                    v[3 * k] = q.x; v[3 * k + 1] = q.y; v[3 * k + 2] = q.z;
+                }
+                tris[f] = make_tri(v, uint32_t(f));
+            }
+            if ((rc = dev_upload(c, tris.data(), tris.size() * sizeof(DTri), &p))) return rc;
+            dm.tris = static_cast<const DTri*>(p);
+            dm.has_tree = 0;
+        }
+    }
+    {
+        std::vector<DSphere> sp(size_t(nspheres) + 1);
+        for (int32_t i = 0; i < nspheres; ++i)
+            sp[size_t(i)] = DSphere{spheres[i].center.x, spheres[i].center.y, spheres[i].center.z,
+                                    spheres[i].radius, spheres[i].material, 0, 0, 0};
+        std::vector<DPlane> pl(size_t(nplanes) + 1);
+        for (int32_t i = 0; i < nplanes; ++i)
+            pl[size_t(i)] = DPlane{planes[i].normal.x, planes[i].normal.y, planes[i].normal.z,
+                                   planes[i].distance, planes[i].material, 0, 0, 0};
+        void* p = nullptr;
+        int rc;
+        if ((rc = dev_upload(c, sp.data(), sp.size() * sizeof(DSphere), &p))) return rc;
+        S.spheres = static_cast<const DSphere*>(p);
+        if ((rc = dev_upload(c, pl.data(), pl.size() * sizeof(DPlane), &p))) return rc;
+        S.planes = static_cast<const DPlane*>(p);
+        S.nspheres = nspheres;
+        S.nplanes = nplanes;
+        if ((rc = dev_upload(c, &S, sizeof(S), &p))) return rc;
+        c->d_scene = static_cast<DScene*>(p);
+    }
+    c->nmodels = nmodels;
+    return ATR_OK;
+}
+
+int atr_scene_info(atr_ctx* c, int64_t* bytes, int32_t* max_nodes, int32_t* max_depth) {
+    if (!c) return ATR_E_INVALID;
+    if (bytes) *bytes = c->scene_bytes;
+    if (max_nodes) *max_nodes = c->max_nodes;
+    if (max_depth) *max_depth = c->max_depth;
+    return ATR_OK;
+}
+
+int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles) {
+    if (!tiles || ntiles <= 0) return 0;
+    int32_t W = 0, H = 0;
+    for (int32_t i = 0; i < ntiles; ++i) {
+        if (tiles[i].max_x + 1 > W) W = tiles[i].max_x + 1;
+        if (tiles[i].max_y + 1 > H) H = tiles[i].max_y + 1;
+    }
+    std::vector<DBlock> b;
+    int64_t n = 0;
+    build_blocks(tiles, ntiles, W, H, b, n);
+    return n;
+}
+
+int64_t atr_packed_pixel_map(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, int64_t* out,
+                             int64_t cap) {
+    if (ntiles < 0 || (ntiles && !tiles) || W <= 0 || H <= 0) return ATR_E_INVALID;
+    std::vector<DBlock> b;
+    int64_t n = 0;
+    build_blocks(tiles, ntiles, W, H, b, n);
+    if (out) {
+        int64_t k = 0;
+        for (const DBlock& blk : b) {
+            const uint64_t m = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+            for (int lane = 0; lane < 64; ++lane)
+                if ((m >> lane) & 1) {
+                    if (k < cap) out[k] = int64_t(blk.y0 + (lane >> 3)) * W + (blk.x0 + (lane & 7));
+                    ++k;
+                }
+        }
+    }
+    return n;
+}
+
+int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                        const atr_frame* fr, uint64_t seed, void* stream, int32_t variant) {
+    if (!c || !cam || !fr || !fr->framebuffer || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+    if (cam->width <= 0 || cam->height <= 0 || cam->width > (1 << 16) || cam->height > (1 << 16)) return ATR_E_INVALID;
+    if (fr->layout != ATR_LAYOUT_IMAGE && fr->layout != ATR_LAYOUT_PACKED) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
+    if (!bs) return rc;
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.blocks = static_cast<const DBlock*>(bs->dev.p);
+    P.nblocks = int32_t(bs->host.size());
+    P.layout = fr->layout;
+    P.framebuffer = fr->framebuffer;
+    P.hit_face = fr->hit_face;
+    P.hit_t = fr->hit_t;
+    P.rgb = fr->rgb;
+    P.ray_casts = fr->ray_casts;
+    P.traced_rays = fr->traced_rays;
+    P.error_flag = c->d_error;
+    const int wave = variant == ATR_KERNEL_LANE ? 0 : 1;  // AUTO -> WAVE
+    HIPCHK(hipEventRecord(c->ev_start, s));
+    HIPCHK(atr_launch_render(P, wave, s));
+    HIPCHK(hipEventRecord(c->ev_stop, s));
+    HIPCHK(hipEventRecord(c->ev_done, s));
+    c->have_render = true;
+    c->last_stream = s;
+    c->last_ntiles = ntiles;
+    return ATR_OK;
+}
+
+int atr_render_start(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                     const atr_frame* fr, uint64_t seed, void* stream) {
+    return atr_render_start_ex(c, cam, tiles, ntiles, fr, seed, stream, ATR_KERNEL_AUTO);
+}
+
+int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
+    if (!c) return ATR_E_INVALID;
+    if (tiles_done) *tiles_done = 0;
+    if (!c->have_render) { return ATR_OK; }
+    HIPCHK(hipSetDevice(c->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(c->ev_done);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return -(1000 + int(q));
+        const auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
+        if (uint32_t(el.count()) >= timeout_ms) return 1;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    int32_t err = 0;
+    HIPCHK(hipMemcpy(&err, c->d_error, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+        HIPCHK(hipMemset(c->d_error, 0, sizeof(int32_t)));
+        return ATR_E_TREE_DEPTH;
+    }
+    if (tiles_done) *tiles_done = c->last_ntiles;
+    return ATR_OK;
+}
+
+int atr_last_kernel_ms(atr_ctx* c, float* ms) {
+    if (!c || !ms || !c->have_render) return ATR_E_INVALID;
+    HIPCHK(hipEventSynchronize(c->ev_stop));
+    HIPCHK(hipEventElapsedTime(ms, c->ev_start, c->ev_stop));
+    return ATR_OK;
+}
+
+int atr_unpack(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width, const uint32_t* packed,
+               uint32_t* image, void* stream) {
+    if (!c || !packed || !image || width <= 0 || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    int32_t H = 0;
+    for (int32_t i = 0; i < ntiles; ++i) if (tiles[i].max_y + 1 > H) H = tiles[i].max_y + 1;
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, width, H, rc);
+    if (!bs) return rc;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    HIPCHK(atr_launch_unpack(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed, image, s));
+    return ATR_OK;
+}
+
+int atr_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width,
+                       const uint32_t* casts, int64_t* out, void* stream) {
+    if (!c || !casts || !out || width <= 0 || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    void* dt = nullptr;
+    HIPCHK(hipMallocAsync(&dt, sizeof(atr_tile) * size_t(ntiles ? ntiles : 1), s));
+    HIPCHK(hipMemcpyAsync(dt, tiles, sizeof(atr_tile) * size_t(ntiles), hipMemcpyHostToDevice, s));
+    HIPCHK(atr_launch_tile_casts(static_cast<const atr_tile*>(dt), ntiles, width, casts, out, s));
+    HIPCHK(hipFreeAsync(dt, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return ATR_OK;
+}
+
+int atr_device_alloc(atr_ctx* c, size_t bytes, void** p) {
+    if (!c || !p) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+    return ATR_OK;
+}
+int atr_device_free(atr_ctx* c, void* p) {
+    if (!c) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipFree(p));
+    return ATR_OK;
+}
+int atr_memcpy_d2h(atr_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c || !dst || !src) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return ATR_OK;
+}
+int atr_memset_d(atr_ctx* c, void* p, int v, size_t bytes) {
+    if (!c || !p) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemset(p, v, bytes));
+    return ATR_OK;
+}
+
+}  // extern "C"

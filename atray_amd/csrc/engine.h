@@ -1,0 +1,142 @@
+// engine.h -- internal types shared by the host side (scene prep, C-ABI) and the HIP kernels.
+// Everything here is plain data; f32 helpers are __host__ __device__ so host-side
+// precomputation and the kernels evaluate the same expressions in the same order
+// (reference op order: PL/PL_math.h:106-123,416-422). Built with -ffp-contract=off.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/atray.h"
+
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#define ATR_HD __host__ __device__ __forceinline__
+#else
+#define ATR_HD inline
+#endif
+
+namespace atr {
+
+constexpr float kMaxFloat = 3.402823466e+38F;     // PL_base_defs.h:72
+constexpr float kInvU32Max = 2.328306437e-10F;    // PL_base_defs.h:75
+constexpr float kTol = 0.0001f;                   // ray.h:5
+constexpr int kMaskLevels = 16;                   // traversal mask-stack depth (8 bits/level)
+constexpr int kMaxMaterials = 32;
+constexpr int kMaxModels = 8;
+
+struct V3 { float x, y, z; };
+ATR_HD V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+ATR_HD V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+ATR_HD V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+ATR_HD V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+ATR_HD V3 scale(V3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+ATR_HD V3 divs(V3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+ATR_HD V3 had(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+ATR_HD float dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+ATR_HD V3 cross(V3 a, V3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+ATR_HD float len2(V3 v) { return (v.x * v.x) + (v.y * v.y) + (v.z * v.z); }
+// normalize (PL_math.h:387-392). SVML _mm_invsqrt_ps is declared as 1/sqrtf.
+ATR_HD V3 unit(V3 v) { float inv = 1.0f / sqrtf(len2(v)); return scale(v, inv); }
+ATR_HD V3 lerp3(V3 s, V3 t, float k) { return add(scale(sub(t, s), k), s); }
+ATR_HD float pl_max(float a, float b) { return a > b ? a : b; }
+ATR_HD float pl_min(float a, float b) { return a > b ? b : a; }
+ATR_HD V3 from(atr_vec3 v) { return mk(v.x, v.y, v.z); }
+
+// PCG-XSH-RR (PL_math.h:506-516)
+ATR_HD uint32_t pcg_next(uint64_t& state, uint64_t stream) {
+    uint64_t old = state;
+    state = old * 6364136223846793005ULL + (stream | 1ULL);
+    uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((0u - rot) & 31u));
+}
+ATR_HD float rand_bi(uint64_t& state, uint64_t stream) {  // PL_math.h:525-541
+    float rd = (float)pcg_next(state, stream) * kInvU32Max;
+    return -1.0f + 2.0f * rd;
+}
+// Per-pixel stream (deviation from renderer.cpp:376-378's rdtsc*thread seeding).
+ATR_HD void pixel_stream(uint64_t seed, int64_t pixel, uint64_t& state, uint64_t& stream) {
+    uint64_t x = seed ^ (uint64_t)pixel;
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    state = x ^ (x >> 31);
+    stream = ((uint64_t)pixel << 1) | 1ULL;
+}
+
+// ---------------------------------------------------------------- device scene layout
+// Octree node, 32 B: two float4 loads. children = children_start_position (0 = leaf),
+// parent = index of the parent node (-1 for the root), used by the stackless DFS.
+struct alignas(16) DNode {
+    float lo_x, lo_y, lo_z, hi_x;
+    float hi_y, hi_z;
+    int32_t children;
+    int32_t parent;
+};
+static_assert(sizeof(DNode) == 32, "DNode layout");
+
+// Leaf primitive / brute-force triangle, 48 B: a, ab = b - a, ac = c - a (the first two
+// subtractions of model.h:77-78, done once on the host: same IEEE f32 results), face index.
+struct alignas(16) DTri {
+    float ax, ay, az, abx;
+    float aby, abz, acx, acy;
+    float acz;
+    uint32_t face;
+    float pad0, pad1;
+};
+static_assert(sizeof(DTri) == 48, "DTri layout");
+
+// Per-model device view. has_tree == 0 selects the brute-force branch (renderer.cpp:58-82).
+struct DModel {
+    const DNode* nodes;          // octree nodes in reference order (root = 0)
+    const uint32_t* leaf_range;  // 2 u32 per node: first DTri, count (leaves only)
+    const DTri* tris;            // leaf-ordered primitives (tree) or face-ordered (brute force)
+    const float* shade;          // 9 f32 per face: smooth -> na, nb, nc; flat -> v0, v1, v2
+    uint32_t nfaces;
+    int32_t has_tree;
+    int32_t root_leaf;           // root never split (kd_tree.cpp:344-361)
+    int32_t smooth;              // normals.size > 0 (renderer.cpp:129)
+    int32_t material;
+    float aabb[6];               // Model::surrounding_aabb
+};
+
+struct DMaterial { float ex, ey, ez, rx, ry, rz, scatter, pad; };
+struct DSphere { float cx, cy, cz, r; int32_t material, pad0, pad1, pad2; };
+struct DPlane { float nx, ny, nz, d; int32_t material, pad0, pad1, pad2; };
+
+// Scene-wide device data, uploaded once by atr_scene_upload (read via scalar loads).
+struct DScene {
+    DMaterial mats[kMaxMaterials];
+    DModel models[kMaxModels];
+    int32_t nmats, nmodels, nspheres, nplanes;
+    const DSphere* spheres;
+    const DPlane* planes;
+};
+
+// A work block: one wavefront, an 8x8 pixel cell at (x0, y0); lane l -> (x0 + (l & 7),
+// y0 + (l >> 3)); only lanes whose bit is set in `mask` own a pixel of the render.
+struct alignas(16) DBlock {
+    int32_t x0, y0;
+    uint32_t mask_lo, mask_hi;
+    int32_t out_base;  // PACKED layout: output slot of the block's first owned pixel
+    int32_t pad[3];
+};
+static_assert(sizeof(DBlock) == 32, "DBlock layout");
+
+// Per-render kernel argument (by value, no dynamic indexing into it).
+struct RenderParams {
+    atr_camera cam;
+    const DScene* scene;
+    uint64_t seed;
+    const DBlock* blocks;
+    int32_t nblocks;
+    int32_t layout;
+    uint32_t* framebuffer;
+    uint32_t* hit_face;
+    float* hit_t;
+    float* rgb;
+    uint32_t* ray_casts;
+    unsigned long long* traced_rays;
+    int32_t* error_flag;  // set to 1 if a ray hit a traversal limit (never for depth <= 16)
+};
+
+}  // namespace atr

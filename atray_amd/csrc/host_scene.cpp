@@ -1,0 +1,367 @@
+// host_scene.cpp -- host prerequisites of the render path (not timed by the benchmark):
+// OBJ loading with the reference's number parser, model AABB/translation, the octree build
+// and its flattening into the device layout of engine.h. Reference: OBJ_loader.cpp:278-360,
+// utilities/parser.h, model.h:41-61,136-152, kd_tree.cpp:1-288, camera.h, renderer.cpp:403-445.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "host_scene.h"
+
+using namespace atr;
+
+namespace {
+
+// ------------------------------------------------------------------ text parsing
+// A cursor over NUL-free OBJ text that always ends in '\n' (OBJ_loader.cpp:330-331 appends one).
+struct Cursor {
+    const char* p;
+    bool at(char c) const { return *p == c; }
+    void skip_blanks() { while (*p == ' ' || *p == '\t' || *p == '\r') ++p; }  // parser.h:4-35
+    void to_next_line() { while (*p != '\n') ++p; ++p; }
+    static bool digit(char c) { return c >= '0' && c <= '9'; }
+
+    // parse_int (parser.h:38-65); int32 overflow wraps (the reference's is UB)
+    int32_t integer() {
+        skip_blanks();
+        uint32_t sgn = 1u;
+        if (*p == '+') ++p;
+        else if (*p == '-') { sgn = 0xFFFFFFFFu; ++p; }
+        uint32_t v = 0;
+        while (digit(*p)) v = v * 10u + uint32_t(*p++ - '0');
+        return int32_t(v * sgn);
+    }
+
+    // parse_f64 (parser.h:113-191): integer mantissa of all digits, one f64 multiply by the
+    // power-of-ten table entry for (exponent - fraction digits), table range 1e-28..1e19.
+    double real() {
+        static const double kPow10[48] = {
+            1.0e-28, 1.0e-27, 1.0e-26, 1.0e-25, 1.0e-24, 1.0e-23, 1.0e-22, 1.0e-21, 1.0e-20, 1.0e-19,
+            1.0e-18, 1.0e-17, 1.0e-16, 1.0e-15, 1.0e-14, 1.0e-13, 1.0e-12, 1.0e-11, 1.0e-10, 1.0e-9,
+            1.0e-8,  1.0e-7,  1.0e-6,  1.0e-5,  1.0e-4,  1.0e-3,  1.0e-2,  1.0e-1,  1.0e0,   1.0e1,
+            1.0e2,   1.0e3,   1.0e4,   1.0e5,   1.0e6,   1.0e7,   1.0e8,   1.0e9,   1.0e10,  1.0e11,
+            1.0e12,  1.0e13,  1.0e14,  1.0e15,  1.0e16,  1.0e17,  1.0e18,  1.0e19};
+        skip_blanks();
+        double sgn = 1.0;
+        if (*p == '+') ++p;
+        else if (*p == '-') { sgn = -1.0; ++p; }
+        uint64_t mant = 0;
+        while (digit(*p)) mant = mant * 10u + uint64_t(*p++ - '0');
+        if (*p == '.') ++p;
+        uint64_t frac = 0;
+        int ndig = 0;
+        while (digit(*p)) { frac = frac * 10u + uint64_t(*p++ - '0'); ++ndig; }
+        uint64_t scale10 = 1;
+        for (int i = 0; i < (ndig > 19 ? 19 : ndig); ++i) scale10 *= 10u;
+        mant = mant * scale10 + frac;
+        int e = 0;
+        if (*p == 'e' || *p == 'E') {
+            ++p;
+            int es = 1;
+            if (*p == '+') ++p;
+            else if (*p == '-') { es = -1; ++p; }
+            while (digit(*p)) e = 10 * e + (*p++ - '0');
+            e *= es;
+        }
+        e -= ndig;
+        double v = double(mant) * sgn;
+        if (e < -28 || e > 19) e = 0;
+        return v * kPow10[e + 28];
+    }
+    V3 vec3() {  // parse_vec3f (parser.h:194-205)
+        float x = float(real());
+        float y = float(real());
+        float z = float(real());
+        return mk(x, y, z);
+    }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ mesh
+int atr::parse_obj_text(const char* text, size_t len, HostMesh& m) {
+    std::string buf(text, len);
+    buf.push_back('\n');
+    for (char& c : buf)
+        if (c == '\0') c = ' ';  // a NUL in the file would end the reference's line scan oddly
+    const char* end = buf.data() + buf.size();
+    Cursor cur{buf.data()};
+    m = HostMesh();
+    while (cur.p < end) {
+        if (cur.at('v')) {  // OBJ_loader.cpp:54-80
+            ++cur.p;
+            if (cur.at(' ')) m.vertices.push_back(cur.vec3());
+            else if (cur.at('t')) { ++cur.p; m.texcoords.push_back(cur.vec3()); }
+            else if (cur.at('n')) { ++cur.p; m.normals.push_back(cur.vec3()); }
+        } else if (cur.at('f')) {  // OBJ_loader.cpp:81-149: first three index groups only
+            ++cur.p;
+            int32_t v[3] = {0, 0, 0}, t[3] = {0, 0, 0}, n[3] = {0, 0, 0};
+            for (int k = 0; k < 3; ++k) {
+                v[k] = cur.integer();
+                if (cur.at('/')) {
+                    ++cur.p;
+                    if (cur.at('/')) { ++cur.p; n[k] = cur.integer(); }
+                    else {
+                        t[k] = cur.integer();
+                        if (cur.at('/')) { ++cur.p; n[k] = cur.integer(); }
+                    }
+                }
+            }
+            for (int k = 0; k < 3; ++k) {
+                m.face_v.push_back(v[k]);
+                m.face_t.push_back(t[k]);
+                m.face_n.push_back(n[k]);
+            }
+        }
+        cur.to_next_line();
+    }
+    // prep_model_data (OBJ_loader.cpp:229-267): relative indices, then drop the +1 offset
+    const int32_t nv = int32_t(m.vertices.size()), nn = int32_t(m.normals.size()),
+                  nt = int32_t(m.texcoords.size());
+    for (size_t i = 0; i < m.face_v.size(); ++i) {
+        if (m.face_t[i] < 0) m.face_t[i] += nt + 1;
+        if (m.face_n[i] < 0) m.face_n[i] += nn + 1;
+        if (m.face_v[i] < 0) m.face_v[i] += nv + 1;
+        m.face_t[i] -= 1;
+        m.face_v[i] -= 1;
+        m.face_n[i] -= 1;
+    }
+    return ATR_OK;
+}
+
+void atr::mesh_aabb(const HostMesh& m, float out[6]) {  // get_AABB (model.h:41-61)
+    float lo[3] = {kMaxFloat, kMaxFloat, kMaxFloat}, hi[3] = {-kMaxFloat, -kMaxFloat, -kMaxFloat};
+    for (const V3& v : m.vertices) {
+        const float c[3] = {v.x, v.y, v.z};
+        for (int a = 0; a < 3; ++a) {
+            hi[a] = pl_max(hi[a], c[a]);
+            lo[a] = pl_min(lo[a], c[a]);
+        }
+    }
+    for (int a = 0; a < 3; ++a) {
+        out[a] = lo[a] - kTol;
+        out[3 + a] = hi[a] + kTol;
+    }
+}
+
+void atr::mesh_translate(HostMesh& m, float box[6], V3 c) {  // translate_to (model.h:136-152)
+    V3 lo = mk(box[0], box[1], box[2]), hi = mk(box[3], box[4], box[5]);
+    V3 old_center = add(lo, divs(sub(hi, lo), 2.0f));
+    V3 d = sub(c, old_center);
+    for (V3& v : m.vertices) v = add(v, d);
+    hi = add(hi, d);
+    lo = add(lo, d);
+    box[0] = lo.x; box[1] = lo.y; box[2] = lo.z;
+    box[3] = hi.x; box[4] = hi.y; box[5] = hi.z;
+}
+
+// ------------------------------------------------------------------ octree
+namespace {
+struct Tri9 { V3 a, b, c; uint32_t face; };
+
+inline bool pt_in(const V3& p, const float* lo, const float* hi) {  // aabb.h:19-27 (closed)
+    return (p.x >= lo[0] && p.x <= hi[0]) && (p.y >= lo[1] && p.y <= hi[1]) &&
+           (p.z >= lo[2] && p.z <= hi[2]);
+}
+}  // namespace
+
+// build_KD_tree (kd_tree.cpp:20-64) + build_oct_kd_tree (kd_tree.cpp:67-288).
+// Node numbering follows the reference exactly: a LIFO work list, children appended as a
+// contiguous block of 8 at the current tree length, in the order bb/bf/tb/tf x left/right.
+int atr::octree_build(const HostMesh& m, uint32_t max_faces, HostTree& T) {
+    struct Work { float lo[3], hi[3]; int32_t children = 0; int32_t parent = -1; int depth = 0;
+                  std::vector<Tri9> prims; };
+    std::vector<Work> nodes(1);
+    float box[6];
+    mesh_aabb(m, box);
+    std::memcpy(nodes[0].lo, box, 12);
+    std::memcpy(nodes[0].hi, box + 3, 12);
+    const size_t nf = m.face_v.size() / 3;
+    nodes[0].prims.resize(nf);
+    for (size_t i = 0; i < nf; ++i) {
+        const int32_t* f = &m.face_v[3 * i];
+        for (int k = 0; k < 3; ++k)
+            if (f[k] < 0 || size_t(f[k]) >= m.vertices.size()) return ATR_E_INVALID;
+        nodes[0].prims[i] = Tri9{m.vertices[f[0]], m.vertices[f[1]], m.vertices[f[2]], uint32_t(i)};
+    }
+    std::vector<int32_t> todo{0};
+    while (!todo.empty()) {
+        const int32_t id = todo.back();
+        todo.pop_back();
+        if (nodes[id].prims.size() <= max_faces || nodes[id].depth >= 64) continue;  // leaf
+        // "SAH" split point = area-weighted centroid (kd_tree.cpp:93-114); f32 sum, f64 area sum
+        V3 acc = mk(0.f, 0.f, 0.f);
+        double area_sum = 0.0;
+        for (const Tri9& t : nodes[id].prims) {
+            V3 centroid = divs(add(add(t.a, t.b), t.c), 3.0f);
+            V3 ab = sub(t.a, t.b), ac = sub(t.a, t.c);
+            float area = std::sqrt(len2(cross(ac, ab))) / 2.0f;  // area_of_triangle (:3-8)
+            acc = add(acc, scale(centroid, area));
+            area_sum += double(area);
+        }
+        const V3 s = divs(acc, float(area_sum));
+        if (!pt_in(s, nodes[id].lo, nodes[id].hi)) continue;  // degenerate split -> leaf
+        const float* L = nodes[id].lo;
+        const float* H = nodes[id].hi;
+        // child k: x from bit 2 (left/right), y from bit 1 (bottom/top), z from bit 0 (back/front)
+        float cb[8][6];
+        for (int k = 0; k < 8; ++k) {
+            const bool xr = (k >> 2) & 1, yt = (k >> 1) & 1, zf = k & 1;
+            cb[k][0] = xr ? s.x : L[0]; cb[k][3] = xr ? H[0] : s.x;
+            cb[k][1] = yt ? s.y : L[1]; cb[k][4] = yt ? H[1] : s.y;
+            cb[k][2] = zf ? s.z : L[2]; cb[k][5] = zf ? H[2] : s.z;
+        }
+        std::vector<Tri9> parts[8];
+        for (const Tri9& t : nodes[id].prims)  // vertex-in-box assignment (:10-17, :181-228)
+            for (int k = 0; k < 8; ++k)
+                if (pt_in(t.a, cb[k], cb[k] + 3) || pt_in(t.b, cb[k], cb[k] + 3) ||
+                    pt_in(t.c, cb[k], cb[k] + 3))
+                    parts[k].push_back(t);
+        const int32_t first = int32_t(nodes.size());
+        const int depth = nodes[id].depth;
+        nodes[id].prims.clear();
+        nodes[id].prims.shrink_to_fit();
+        nodes[id].children = first;
+        for (int k = 0; k < 8; ++k) {
+            Work w;
+            std::memcpy(w.lo, cb[k], 12);
+            std::memcpy(w.hi, cb[k] + 3, 12);
+            w.parent = id;
+            w.depth = depth + 1;
+            w.prims.swap(parts[k]);
+            nodes.push_back(std::move(w));
+        }
+        for (int k = 0; k < 8; ++k) todo.push_back(first + k);
+    }
+    T = HostTree();
+    T.nnodes = int32_t(nodes.size());
+    T.bounds.resize(6 * nodes.size());
+    T.children.resize(nodes.size());
+    T.parent.resize(nodes.size());
+    T.leaf_first.assign(nodes.size(), 0);
+    T.leaf_count.assign(nodes.size(), 0);
+    T.depth.resize(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        std::memcpy(&T.bounds[6 * i], nodes[i].lo, 12);
+        std::memcpy(&T.bounds[6 * i + 3], nodes[i].hi, 12);
+        T.children[i] = nodes[i].children;
+        T.parent[i] = nodes[i].parent;
+        T.depth[i] = nodes[i].depth;
+        if (nodes[i].children == 0) {
+            T.leaf_first[i] = uint32_t(T.prim_face.size());
+            T.leaf_count[i] = uint32_t(nodes[i].prims.size());
+            for (const Tri9& t : nodes[i].prims) {
+                const float v[9] = {t.a.x, t.a.y, t.a.z, t.b.x, t.b.y, t.b.z, t.c.x, t.c.y, t.c.z};
+                T.prim_vertices.insert(T.prim_vertices.end(), v, v + 9);
+                T.prim_face.push_back(t.face);
+            }
+        }
+    }
+    return ATR_OK;
+}
+
+int atr::octree_finish(HostTree& T) {  // parents/depths for a caller-provided tree
+    const int32_t n = T.nnodes;
+    T.parent.assign(size_t(n), -1);
+    T.depth.assign(size_t(n), 0);
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t c = T.children[size_t(i)];
+        if (c == 0) continue;
+        if (c < 0 || c + 8 > n) return ATR_E_INVALID;
+        for (int k = 0; k < 8; ++k) T.parent[size_t(c + k)] = i;
+    }
+    for (int32_t i = 0; i < n; ++i) {  // depth by walking parents (children follow parents)
+        int d = 0;
+        for (int32_t p = T.parent[size_t(i)]; p >= 0; p = T.parent[size_t(p)]) {
+            if (++d > n) return ATR_E_INVALID;  // cycle
+        }
+        T.depth[size_t(i)] = d;
+    }
+    return ATR_OK;
+}
+
+void atr::octree_stats(const HostTree& T, int64_t s[7]) {
+    int64_t inner = 0, leaves = 0, empty = 0, refs = 0, maxleaf = 0, depth = 0;
+    for (int32_t i = 0; i < T.nnodes; ++i) {
+        if (T.children[size_t(i)]) { ++inner; }
+        else {
+            ++leaves;
+            const int64_t c = T.leaf_count[size_t(i)];
+            refs += c;
+            if (!c) ++empty;
+            if (c > maxleaf) maxleaf = c;
+        }
+        if (T.depth[size_t(i)] > depth) depth = T.depth[size_t(i)];
+    }
+    s[0] = T.nnodes; s[1] = inner; s[2] = leaves; s[3] = empty; s[4] = refs; s[5] = maxleaf; s[6] = depth;
+}
+
+// ------------------------------------------------------------------ camera / tiles
+void atr::camera_set(atr_camera& cm, V3 eye, V3 facing, int32_t w, int32_t h, int32_t aa,
+                     uint32_t spp, int32_t bounces, float h_fov) {  // set_camera (camera.h:23-45)
+    std::memset(&cm, 0, sizeof(cm));
+    cm.h_fov = h_fov;
+    cm.width = w;
+    cm.height = h;
+    cm.anti_aliasing = aa;
+    cm.samples_per_pixel = spp;
+    cm.bounce_limit = bounces;
+    cm.aspect_ratio = float(w) / float(h);
+    const V3 f = unit(facing);
+    const V3 fc = add(eye, f);
+    const V3 z = neg(f);
+    const V3 x = unit(cross(mk(0.f, 1.f, 0.f), z));
+    const V3 y = unit(cross(z, x));
+    cm.eye = atr_vec3{eye.x, eye.y, eye.z};
+    cm.frame_center = atr_vec3{fc.x, fc.y, fc.z};
+    cm.camera_z = atr_vec3{z.x, z.y, z.z};
+    cm.camera_x = atr_vec3{x.x, x.y, x.z};
+    cm.camera_y = atr_vec3{y.x, y.y, y.z};
+    cm.half_pixel_width = (0.5f * cm.h_fov) / float(w);
+    cm.half_pixel_height = 0.5f / float(h);
+}
+
+int32_t atr::reference_tiles(int32_t W, int32_t H, int32_t threads, atr_tile* out, int32_t cap) {
+    if (W <= 0 || H <= 0 || threads <= 0) return 0;
+    int32_t side = W / threads;  // renderer.cpp:406-411
+    if (side > H) side = H / threads;
+    if (side <= 0) side = 1;
+    const int32_t nx = (W + side - 1) / side, ny = (H + side - 1) / side;
+    int32_t n = 0;
+    for (int32_t ty = 0; ty < ny; ++ty)
+        for (int32_t tx = 0; tx < nx; ++tx, ++n) {
+            if (n >= cap) continue;
+            atr_tile t;
+            t.min_x = tx * side;
+            t.min_y = ty * side;
+            t.max_x = t.min_x + side < W - 1 ? t.min_x + side : W - 1;  // inclusive, clipped
+            t.max_y = t.min_y + side < H - 1 ? t.min_y + side : H - 1;
+            out[n] = t;
+        }
+    return n;
+}
+
+int32_t atr::shard_tiles(int32_t W, int32_t H, int32_t side, int32_t rank, int32_t world,
+                         atr_tile* out, int32_t cap) {
+    if (W <= 0 || H <= 0 || side <= 0 || world <= 0 || rank < 0 || rank >= world) return 0;
+    const int32_t nx = (W + side - 1) / side, ny = (H + side - 1) / side;
+    int32_t n = 0, k = 0;
+    for (int32_t ty = 0; ty < ny; ++ty)
+        for (int32_t tx = 0; tx < nx; ++tx, ++k) {
+            if (k % world != rank) continue;
+            if (n < cap) {
+                atr_tile t;
+                t.min_x = tx * side;
+                t.min_y = ty * side;
+                t.max_x = (tx + 1) * side - 1 < W - 1 ? (tx + 1) * side - 1 : W - 1;
+                t.max_y = (ty + 1) * side - 1 < H - 1 ? (ty + 1) * side - 1 : H - 1;
+                out[n] = t;
+            }
+            ++n;
+        }
+    return n;
+}

@@ -1,0 +1,45 @@
+// host_scene.h -- host-side scene types behind the opaque atr_mesh / atr_octree handles.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "engine.h"
+
+namespace atr {
+
+// ModelData (model.h:15-23), 0-based indices, 3 ints per face in each index array.
+struct HostMesh {
+    std::vector<V3> vertices, normals, texcoords;
+    std::vector<int32_t> face_v, face_t, face_n;
+    size_t nfaces() const { return face_v.size() / 3; }
+};
+
+// KD_Tree flattened in reference node order, plus parent/depth for the device traversal.
+struct HostTree {
+    int32_t nnodes = 0;
+    std::vector<float> bounds;        // 6 per node
+    std::vector<int32_t> children;    // children_start_position, 0 = leaf
+    std::vector<int32_t> parent;      // -1 for the root
+    std::vector<int32_t> depth;
+    std::vector<uint32_t> leaf_first, leaf_count;
+    std::vector<float> prim_vertices; // 9 per leaf primitive
+    std::vector<uint32_t> prim_face;
+};
+
+int parse_obj_text(const char* text, size_t len, HostMesh& m);
+void mesh_aabb(const HostMesh& m, float out[6]);
+void mesh_translate(HostMesh& m, float box[6], V3 c);
+int octree_build(const HostMesh& m, uint32_t max_faces, HostTree& T);
+int octree_finish(HostTree& T);
+void octree_stats(const HostTree& T, int64_t s[7]);
+void camera_set(atr_camera& cm, V3 eye, V3 facing, int32_t w, int32_t h, int32_t aa, uint32_t spp,
+                int32_t bounces, float h_fov);
+int32_t reference_tiles(int32_t W, int32_t H, int32_t threads, atr_tile* out, int32_t cap);
+int32_t shard_tiles(int32_t W, int32_t H, int32_t side, int32_t rank, int32_t world, atr_tile* out,
+                    int32_t cap);
+
+}  // namespace atr
+
+struct atr_mesh { atr::HostMesh m; };
+struct atr_octree { atr::HostTree t; };

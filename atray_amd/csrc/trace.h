@@ -1,0 +1,243 @@
+// trace.h -- device-side ray/box/triangle math and the exact octree traversal.
+//
+// Semantics are the reference's, bit for bit (kd_tree.cpp:337-465, aabb.h:29-93,
+// model.h:75-103, renderer.cpp:34-160). What changes is HOW the GPU walks the tree:
+//
+//  * no per-ray memory: the reference's DFS hit stack becomes an 8-bit "inner children
+//    still to visit" mask per tree level packed into two u64 registers (16 levels), with
+//    parent indices stored in the nodes for the ascent;
+//  * the reference's insertion-sorted leaf list becomes a K-entry register buffer of the
+//    K smallest (entry distance, discovery index) leaves; a ray that scans K leaves without
+//    a hit re-walks the tree for the next K (ties and order identical to the stable
+//    insertion sort at kd_tree.cpp:392-410, whose order is exactly that key).
+#pragma once
+#include "engine.h"
+
+namespace atr {
+
+struct Ray {
+    V3 o, d, inv;
+    int s0, s1, s2;  // inv_signs (renderer.cpp:41-44)
+};
+
+__device__ __forceinline__ Ray make_ray(V3 o, V3 d) {
+    Ray r;
+    r.o = o;
+    r.d = d;
+    r.inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+    r.s0 = r.inv.x < 0;
+    r.s1 = r.inv.y < 0;
+    r.s2 = r.inv.z < 0;
+    return r;
+}
+
+struct NodeBox { float lx, ly, lz, hx, hy, hz; int32_t children, parent; };
+
+__device__ __forceinline__ NodeBox load_node(const DNode* __restrict__ nodes, int32_t i) {
+    const float4* p = reinterpret_cast<const float4*>(nodes + i);
+    const float4 a = p[0], b = p[1];
+    NodeBox n;
+    n.lx = a.x; n.ly = a.y; n.lz = a.z; n.hx = a.w;
+    n.hy = b.x; n.hz = b.y;
+    n.children = __float_as_int(b.z);
+    n.parent = __float_as_int(b.w);
+    return n;
+}
+
+// check_ray_AABB_intersection (aabb.h:65-93): no z merge, no t > 0 requirement.
+__device__ __forceinline__ bool box_check(const Ray& r, float lx, float ly, float lz, float hx,
+                                          float hy, float hz) {
+    float tmin = ((r.s0 ? hx : lx) - r.o.x) * r.inv.x;
+    float tmax = ((r.s0 ? lx : hx) - r.o.x) * r.inv.x;
+    const float tymin = ((r.s1 ? hy : ly) - r.o.y) * r.inv.y;
+    const float tymax = ((r.s1 ? ly : hy) - r.o.y) * r.inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((r.s2 ? hz : lz) - r.o.z) * r.inv.z;
+    const float tzmax = ((r.s2 ? lz : hz) - r.o.z) * r.inv.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    return true;
+}
+
+// get_ray_AABB_intersection (aabb.h:29-63): entry t, else exit t (origin inside), else 0.
+__device__ __forceinline__ float box_entry(const Ray& r, float lx, float ly, float lz, float hx,
+                                           float hy, float hz) {
+    float tmin = ((r.s0 ? hx : lx) - r.o.x) * r.inv.x;
+    float tmax = ((r.s0 ? lx : hx) - r.o.x) * r.inv.x;
+    const float tymin = ((r.s1 ? hy : ly) - r.o.y) * r.inv.y;
+    const float tymax = ((r.s1 ? ly : hy) - r.o.y) * r.inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return 0;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((r.s2 ? hz : lz) - r.o.z) * r.inv.z;
+    const float tzmax = ((r.s2 ? lz : hz) - r.o.z) * r.inv.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return 0;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    if (tmin > 0) return tmin;
+    if (tmax > 0) return tmax;
+    return 0;
+}
+
+struct TriRec { V3 a, ab, ac; uint32_t face; };
+
+__device__ __forceinline__ TriRec load_tri(const DTri* __restrict__ tris, uint32_t i) {
+    const float4* p = reinterpret_cast<const float4*>(tris + i);
+    const float4 q0 = p[0], q1 = p[1], q2 = p[2];
+    TriRec t;
+    t.a = mk(q0.x, q0.y, q0.z);
+    t.ab = mk(q0.w, q1.x, q1.y);
+    t.ac = mk(q1.z, q1.w, q2.x);
+    t.face = __float_as_uint(q2.y);
+    return t;
+}
+
+// get_triangle_ray_intersection_culled (model.h:75-103); ab/ac precomputed on the host.
+__device__ __forceinline__ float tri_hit(const Ray& r, V3 a, V3 ab, V3 ac, float& u, float& v) {
+    const V3 pvec = cross(r.d, ac);
+    const float det = dot(ab, pvec);
+    if (det < kTol) return 0;
+    const float det_inv = 1 / det;
+    const V3 tvec = sub(r.o, a);
+    u = dot(tvec, pvec) * det_inv;
+    if (u < 0 || u > 1) return 0;
+    const V3 qvec = cross(tvec, ab);
+    v = dot(r.d, qvec) * det_inv;
+    if (v < 0 || u + v > 1) return 0;
+    return dot(qvec, ac) * det_inv;
+}
+
+struct Hit {
+    float t;      // closest accepted distance (kMaxFloat = none)
+    uint32_t face;
+    float u, v;
+};
+
+// Scan one leaf's primitives in leaf order (kd_tree.cpp:440-456). True if `h` improved.
+__device__ __forceinline__ bool scan_leaf(const Ray& r, const DTri* __restrict__ tris, uint32_t first,
+                                          uint32_t count, Hit& h) {
+    bool improved = false;
+    for (uint32_t k = 0; k < count; ++k) {
+        const TriRec t = load_tri(tris, first + k);
+        float u = 0.f, v = 0.f;
+        const float dist = tri_hit(r, t.a, t.ab, t.ac, u, v);
+        if (dist < h.t && dist > kTol) {
+            h.t = dist;
+            h.face = t.face;
+            h.u = u;
+            h.v = v;
+            improved = true;
+        }
+    }
+    return improved;
+}
+
+// ------------------------------------------------------------------ leaf order buffer
+template <int K>
+struct LeafBuf {
+    float d[K];
+    int32_t node[K];
+    int32_t idx[K];
+};
+
+template <int K>
+__device__ __forceinline__ void lb_clear(LeafBuf<K>& b) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { b.d[j] = __builtin_inff(); b.node[j] = 0; b.idx[j] = 0; }
+}
+
+// Insert a leaf discovered after every entry already held (larger discovery index): it goes
+// behind every entry with distance <= dis, as the stable insertion sort does.
+template <int K>
+__device__ __forceinline__ void lb_insert(LeafBuf<K>& b, float dis, int32_t node, int32_t idx) {
+    if (!(dis < b.d[K - 1])) return;
+    b.d[K - 1] = dis;
+    b.node[K - 1] = node;
+    b.idx[K - 1] = idx;
+#pragma unroll
+    for (int j = K - 1; j > 0; --j) {
+        if (b.d[j] < b.d[j - 1]) {
+            const float td = b.d[j]; b.d[j] = b.d[j - 1]; b.d[j - 1] = td;
+            const int32_t tn = b.node[j]; b.node[j] = b.node[j - 1]; b.node[j - 1] = tn;
+            const int32_t ti = b.idx[j]; b.idx[j] = b.idx[j - 1]; b.idx[j - 1] = ti;
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ int32_t lb_node(const LeafBuf<K>& b, int j) {
+    int32_t r = b.node[0];
+#pragma unroll
+    for (int q = 1; q < K; ++q) r = (j == q) ? b.node[q] : r;
+    return r;
+}
+
+// Examine the children of an inner node (kd_tree.cpp:370-434): box-test children in order
+// until 5 have been hit; inner hits -> returned bit mask, leaf hits -> leaf order buffer.
+template <int K>
+__device__ __forceinline__ uint32_t examine_children(const Ray& r, const DNode* __restrict__ nodes,
+                                                     int32_t first, LeafBuf<K>& lb, int32_t& disc,
+                                                     int32_t& ncand, float bd, int32_t bi) {
+    uint32_t mask = 0;
+    int nodes_hit = 0;
+    for (int i = 0; i < 8 && nodes_hit <= 4; ++i) {
+        const NodeBox c = load_node(nodes, first + i);
+        if (c.children != 0) {
+            if (box_check(r, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz)) {
+                ++nodes_hit;
+                mask |= 1u << i;
+            }
+        } else {
+            const float dis = box_entry(r, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz);
+            if (dis > 0.0f) {
+                ++nodes_hit;
+                const int32_t id = disc++;
+                if (dis > bd || (dis == bd && id > bi)) {
+                    ++ncand;
+                    lb_insert<K>(lb, dis, first + i, id);
+                }
+            }
+        }
+    }
+    return mask;
+}
+
+// One DFS pass over the inner nodes (the reference's hit-stack loop, kd_tree.cpp:363-435),
+// keeping the K first leaves (in sorted order) strictly after (bd, bi). Returns the number of
+// candidate leaves after the bound, or -1 if the tree is deeper than the mask stack.
+template <int K>
+__device__ __forceinline__ int32_t traverse_pass(const Ray& r, const DNode* __restrict__ nodes,
+                                                 LeafBuf<K>& lb, float bd, int32_t bi) {
+    lb_clear<K>(lb);
+    int32_t disc = 0, ncand = 0;
+    const NodeBox root = load_node(nodes, 0);
+    uint64_t lo = examine_children<K>(r, nodes, root.children, lb, disc, ncand, bd, bi);
+    uint64_t hi = 0;
+    int32_t p = 0, pfirst = root.children, lvl = 0;
+    for (;;) {
+        const uint32_t m = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
+        if (m) {
+            const int s = 31 - __clz(m);
+            if (lvl < 8) lo &= ~(uint64_t(1) << (8 * lvl + s));
+            else hi &= ~(uint64_t(1) << (8 * (lvl - 8) + s));
+            const int32_t c = pfirst + s;
+            const NodeBox cn = load_node(nodes, c);
+            const uint64_t cm = examine_children<K>(r, nodes, cn.children, lb, disc, ncand, bd, bi);
+            ++lvl;
+            if (lvl >= kMaskLevels) return -1;
+            if (lvl < 8) lo |= cm << (8 * lvl);
+            else hi |= cm << (8 * (lvl - 8));
+            p = c;
+            pfirst = cn.children;
+        } else {
+            if (lvl == 0) break;
+            --lvl;
+            p = load_node(nodes, p).parent;
+            pfirst = load_node(nodes, p).children;
+        }
+    }
+    return ncand;
+}
+
+}  // namespace atr

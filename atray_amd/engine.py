@@ -1,0 +1,368 @@
+"""ctypes binding of the C-ABI in ``include/atray.h`` (``atray_amd/_lib/libatray_hip.so``).
+
+The HIP library is the product path: there is no CPU fallback. Loading fails loudly if the
+library was not built (``__graft_entry__.build()`` / ``make -C atray_amd/csrc``).
+
+torch is imported before the library is loaded so that both bind the same HIP runtime
+(torch's bundled ``libamdhip64.so`` carries the SONAME ``libamdhip64.so.7`` that the library
+needs); torch then provides device memory, streams and ``torch.distributed`` (RCCL).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libatray_hip.so")
+
+ATR_LAYOUT_IMAGE = 0
+ATR_LAYOUT_PACKED = 1
+ATR_KERNEL_AUTO, ATR_KERNEL_LANE, ATR_KERNEL_WAVE = 0, 1, 2
+MISS = 0xFFFFFFFF
+MAX_FLOAT = np.float32(3.402823466e38)
+
+ERRORS = {-1: "ATR_E_INVALID", -2: "ATR_E_IO", -3: "ATR_E_NOMEM", -4: "ATR_E_NOSCENE",
+          -5: "ATR_E_TREE_DEPTH"}
+
+
+class AtrError(RuntimeError):
+    pass
+
+
+def check(rc, what=""):
+    if rc < 0:
+        name = ERRORS.get(rc) or (f"hipError {-rc - 1000}" if rc <= -1000 else str(rc))
+        raise AtrError(f"{what}: {name}")
+    return rc
+
+
+class atr_vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class atr_material(C.Structure):
+    _fields_ = [("emission", atr_vec3), ("reflection", atr_vec3), ("scatter", C.c_float)]
+
+
+class atr_model(C.Structure):
+    _fields_ = [("mesh", C.c_void_p), ("tree", C.c_void_p), ("surrounding_aabb", C.c_float * 6),
+                ("material", C.c_int32)]
+
+
+class atr_sphere(C.Structure):
+    _fields_ = [("center", atr_vec3), ("radius", C.c_float), ("material", C.c_int32)]
+
+
+class atr_plane(C.Structure):
+    _fields_ = [("normal", atr_vec3), ("distance", C.c_float), ("material", C.c_int32)]
+
+
+class atr_camera(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("anti_aliasing", C.c_int32),
+                ("samples_per_pixel", C.c_uint32), ("bounce_limit", C.c_int32),
+                ("aspect_ratio", C.c_float), ("camera_z", atr_vec3), ("camera_x", atr_vec3),
+                ("camera_y", atr_vec3), ("eye", atr_vec3), ("frame_center", atr_vec3),
+                ("h_fov", C.c_float), ("half_pixel_width", C.c_float),
+                ("half_pixel_height", C.c_float)]
+
+
+class atr_tile(C.Structure):
+    _fields_ = [("min_x", C.c_int32), ("min_y", C.c_int32), ("max_x", C.c_int32),
+                ("max_y", C.c_int32)]
+
+
+class atr_frame(C.Structure):
+    _fields_ = [("layout", C.c_int32), ("framebuffer", C.c_void_p), ("hit_face", C.c_void_p),
+                ("hit_t", C.c_void_p), ("rgb", C.c_void_p), ("ray_casts", C.c_void_p),
+                ("traced_rays", C.c_void_p)]
+
+
+# every symbol include/atray.h declares (checked by tests/test_capi_symbols.py)
+EXPORTS = [
+    "atr_mesh_load_obj", "atr_mesh_parse_obj", "atr_mesh_from_arrays", "atr_mesh_free",
+    "atr_mesh_info", "atr_mesh_aabb", "atr_mesh_translate_to", "atr_octree_build",
+    "atr_octree_from_nodes", "atr_octree_free", "atr_octree_export", "atr_octree_stats", "atr_camera_set",
+    "atr_make_tiles", "atr_make_shard_tiles", "atr_create", "atr_destroy", "atr_version",
+    "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
+    "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
+    "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
+    "atr_memset_d",
+]
+
+_lib = None
+
+
+def lib():
+    """Load the HIP engine library (torch first: shared HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (binds libamdhip64.so.7 before our library needs it)
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"atray HIP engine not built: {LIB_PATH} missing "
+                          "(run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, vp, i32, u32, i64 = C.POINTER, C.c_void_p, C.c_int32, C.c_uint32, C.c_int64
+    sig = {
+        "atr_mesh_load_obj": ([C.c_char_p, P(vp)], C.c_int),
+        "atr_mesh_parse_obj": ([C.c_char_p, C.c_size_t, P(vp)], C.c_int),
+        "atr_mesh_from_arrays": ([vp, u32, vp, u32, vp, u32, vp, P(vp)], C.c_int),
+        "atr_mesh_free": ([vp], None),
+        "atr_mesh_info": ([vp, P(u32), P(u32), P(u32)], C.c_int),
+        "atr_mesh_aabb": ([vp, C.c_float * 6], C.c_int),
+        "atr_mesh_translate_to": ([vp, C.c_float * 6, atr_vec3], C.c_int),
+        "atr_octree_build": ([vp, u32, P(vp)], C.c_int),
+        "atr_octree_from_nodes": ([i32, vp, vp, vp, vp, u32, vp, vp, P(vp)], C.c_int),
+        "atr_octree_free": ([vp], None),
+        "atr_octree_export": ([vp, vp, vp, vp, vp, vp, vp], C.c_int),
+        "atr_octree_stats": ([vp, i64 * 7], C.c_int),
+        "atr_camera_set": ([P(atr_camera), atr_vec3, atr_vec3, i32, i32, i32, u32, i32, C.c_float], C.c_int),
+        "atr_make_tiles": ([i32, i32, i32, vp, i32], i32),
+        "atr_make_shard_tiles": ([i32, i32, i32, i32, i32, vp, i32], i32),
+        "atr_create": ([C.c_int, P(vp)], C.c_int),
+        "atr_destroy": ([vp], C.c_int),
+        "atr_version": ([], C.c_char_p),
+        "atr_scene_upload": ([vp, vp, i32, vp, i32, vp, i32, vp, i32], C.c_int),
+        "atr_scene_info": ([vp, P(i64), P(i32), P(i32)], C.c_int),
+        "atr_render_start": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp], C.c_int),
+        "atr_render_start_ex": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32], C.c_int),
+        "atr_render_packed_size": ([vp, i32], i64),
+        "atr_packed_pixel_map": ([vp, i32, i32, i32, vp, i64], i64),
+        "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
+        "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
+        "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
+        "atr_last_kernel_ms": ([vp, P(C.c_float)], C.c_int),
+        "atr_device_alloc": ([vp, C.c_size_t, P(vp)], C.c_int),
+        "atr_device_free": ([vp, vp], C.c_int),
+        "atr_memcpy_d2h": ([vp, vp, vp, C.c_size_t], C.c_int),
+        "atr_memset_d": ([vp, vp, C.c_int, C.c_size_t], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def vec3(t):
+    return atr_vec3(float(t[0]), float(t[1]), float(t[2]))
+
+
+def tiles_array(tiles):
+    """(n, 4) int array of inclusive rects -> ctypes atr_tile array."""
+    t = np.ascontiguousarray(np.asarray(tiles, dtype=np.int32).reshape(-1, 4))
+    arr = (atr_tile * max(1, len(t)))()
+    C.memmove(arr, t.ctypes.data, t.nbytes)
+    return arr, len(t)
+
+
+def make_tiles(width, height, threads):
+    """Reference tile grid (renderer.cpp:406-445)."""
+    L = lib()
+    n = L.atr_make_tiles(width, height, threads, None, 0)
+    buf = (atr_tile * max(1, n))()
+    L.atr_make_tiles(width, height, threads, C.cast(buf, C.c_void_p), n)
+    return np.array([[t.min_x, t.min_y, t.max_x, t.max_y] for t in buf[:n]], np.int32).reshape(-1, 4)
+
+
+def make_shard_tiles(width, height, side, rank, world):
+    L = lib()
+    n = L.atr_make_shard_tiles(width, height, side, rank, world, None, 0)
+    buf = (atr_tile * max(1, n))()
+    L.atr_make_shard_tiles(width, height, side, rank, world, C.cast(buf, C.c_void_p), n)
+    return np.array([[t.min_x, t.min_y, t.max_x, t.max_y] for t in buf[:n]], np.int32).reshape(-1, 4)
+
+
+class Mesh:
+    """ModelData (model.h:15-23) held by the engine library."""
+
+    def __init__(self, handle):
+        self.h = C.c_void_p(handle)
+
+    @classmethod
+    def load_obj(cls, path):
+        h = C.c_void_p()
+        check(lib().atr_mesh_load_obj(os.fsencode(path), C.byref(h)), f"load {path}")
+        return cls(h.value)
+
+    @classmethod
+    def parse_obj(cls, text):
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        h = C.c_void_p()
+        check(lib().atr_mesh_parse_obj(b, len(b), C.byref(h)), "parse obj")
+        return cls(h.value)
+
+    def info(self):
+        nv, nn, nf = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().atr_mesh_info(self.h, C.byref(nv), C.byref(nn), C.byref(nf)))
+        return nv.value, nn.value, nf.value
+
+    def aabb(self):
+        box = (C.c_float * 6)()
+        check(lib().atr_mesh_aabb(self.h, box))
+        return np.array(list(box), np.float32)
+
+    def translate_to(self, aabb, center):
+        box = (C.c_float * 6)(*[float(x) for x in aabb])
+        check(lib().atr_mesh_translate_to(self.h, box, vec3(center)))
+        return np.array(list(box), np.float32)
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value and _lib is not None:
+            _lib.atr_mesh_free(self.h)
+            self.h = None
+
+
+class Octree:
+    """KD_Tree (kd_tree.h:38-47): the reference's 8-ary octree, built on the host."""
+
+    def __init__(self, handle):
+        self.h = C.c_void_p(handle)
+
+    @classmethod
+    def build(cls, mesh: Mesh, max_faces=300):
+        h = C.c_void_p()
+        check(lib().atr_octree_build(mesh.h, int(max_faces), C.byref(h)), "octree build")
+        return cls(h.value)
+
+    @classmethod
+    def from_nodes(cls, bounds, children, leaf_first, leaf_count, prim_vertices, prim_face):
+        bounds = np.ascontiguousarray(bounds, np.float32)
+        children = np.ascontiguousarray(children, np.int32)
+        leaf_first = np.ascontiguousarray(leaf_first, np.uint32)
+        leaf_count = np.ascontiguousarray(leaf_count, np.uint32)
+        prim_vertices = np.ascontiguousarray(prim_vertices, np.float32)
+        prim_face = np.ascontiguousarray(prim_face, np.uint32)
+        h = C.c_void_p()
+        check(lib().atr_octree_from_nodes(len(children), bounds.ctypes.data, children.ctypes.data,
+                                          leaf_first.ctypes.data, leaf_count.ctypes.data,
+                                          len(prim_face), prim_vertices.ctypes.data,
+                                          prim_face.ctypes.data, C.byref(h)), "octree from nodes")
+        return cls(h.value)
+
+    def export(self):
+        st = self.stats()
+        n, p = st["nodes"], st["leaf_prim_refs"]
+        bounds = np.zeros((n, 6), np.float32)
+        children = np.zeros(n, np.int32)
+        first = np.zeros(n, np.uint32)
+        count = np.zeros(n, np.uint32)
+        verts = np.zeros((max(p, 1), 9), np.float32)
+        face = np.zeros(max(p, 1), np.uint32)
+        check(lib().atr_octree_export(self.h, bounds.ctypes.data, children.ctypes.data,
+                                      first.ctypes.data, count.ctypes.data, verts.ctypes.data,
+                                      face.ctypes.data), "octree export")
+        return bounds, children, first, count, verts[:p], face[:p]
+
+    def stats(self):
+        s = (C.c_int64 * 7)()
+        check(lib().atr_octree_stats(self.h, s))
+        keys = ["nodes", "inner", "leaves", "empty_leaves", "leaf_prim_refs", "max_leaf", "depth"]
+        return dict(zip(keys, [int(x) for x in s]))
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value and _lib is not None:
+            _lib.atr_octree_free(self.h)
+            self.h = None
+
+
+def camera(width, height, spp=1, bounces=1, aa=False, eye=(0.1, 2.0, 0.0),
+           facing=(-0.1, -0.5, -1.0), h_fov=1.0):
+    """set_camera (camera.h:40-45); defaults are the app's (app.cpp:81-88)."""
+    cm = atr_camera()
+    check(lib().atr_camera_set(C.byref(cm), vec3(eye), vec3(facing), int(width), int(height),
+                               int(bool(aa)), int(spp), int(bounces), float(h_fov)), "camera")
+    return cm
+
+
+class Engine:
+    """One device context (atr_ctx): scene upload + renders on a HIP stream."""
+
+    def __init__(self, device=0):
+        self.h = C.c_void_p()
+        check(lib().atr_create(int(device), C.byref(self.h)), "atr_create")
+        self.device = device
+        self._keep = []
+
+    def upload(self, materials, models, spheres=(), planes=()):
+        """materials: [(emission, reflection, scatter)], models: [(Mesh, Octree|None, aabb6, mat)]."""
+        mats = (atr_material * len(materials))(
+            *[atr_material(vec3(e), vec3(r), float(s)) for e, r, s in materials])
+        mods = (atr_model * max(1, len(models)))()
+        for i, (mesh, tree, aabb, mat) in enumerate(models):
+            mods[i].mesh = mesh.h.value
+            mods[i].tree = tree.h.value if tree is not None else None
+            for k in range(6):
+                mods[i].surrounding_aabb[k] = float(aabb[k])
+            mods[i].material = int(mat)
+        sph = (atr_sphere * max(1, len(spheres)))(
+            *[atr_sphere(vec3(c), float(r), int(m)) for c, r, m in spheres])
+        pln = (atr_plane * max(1, len(planes)))(
+            *[atr_plane(vec3(n), float(d), int(m)) for n, d, m in planes])
+        check(lib().atr_scene_upload(self.h, C.cast(mats, C.c_void_p), len(materials),
+                                     C.cast(mods, C.c_void_p), len(models),
+                                     C.cast(sph, C.c_void_p), len(spheres),
+                                     C.cast(pln, C.c_void_p), len(planes)), "scene upload")
+        self._keep = [materials, models]
+
+    def scene_info(self):
+        b, n, d = C.c_int64(), C.c_int32(), C.c_int32()
+        check(lib().atr_scene_info(self.h, C.byref(b), C.byref(n), C.byref(d)))
+        return {"device_bytes": b.value, "max_nodes": n.value, "max_depth": d.value}
+
+    def render_start(self, cam, tiles, frame: atr_frame, seed, stream=None, variant=ATR_KERNEL_AUTO):
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_render_start_ex(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n,
+                                        C.byref(frame), C.c_uint64(seed & (2**64 - 1)),
+                                        C.c_void_p(stream) if stream else None, int(variant)),
+              "render start")
+
+    def wait(self, timeout_ms=0xFFFFFFFF):
+        done = C.c_int32()
+        rc = check(lib().atr_render_wait(self.h, int(timeout_ms), C.byref(done)), "render wait")
+        return rc, done.value
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        check(lib().atr_last_kernel_ms(self.h, C.byref(ms)))
+        return ms.value
+
+    def unpack(self, tiles, width, packed_ptr, image_ptr, stream=None):
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_unpack(self.h, C.cast(arr, C.c_void_p), n, int(width), C.c_void_p(packed_ptr),
+                               C.c_void_p(image_ptr), C.c_void_p(stream) if stream else None), "unpack")
+
+    def tile_ray_casts(self, tiles, width, casts_ptr, out_ptr, stream=None):
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_tile_ray_casts(self.h, C.cast(arr, C.c_void_p), n, int(width),
+                                       C.c_void_p(casts_ptr), C.c_void_p(out_ptr),
+                                       C.c_void_p(stream) if stream else None), "tile casts")
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().atr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def packed_size(tiles):
+    arr, n = tiles_array(tiles)
+    return int(lib().atr_render_packed_size(C.cast(arr, C.c_void_p), n))
+
+
+def packed_pixel_map(tiles, width, height):
+    """Pixel index of every slot of a PACKED render of `tiles` (host-only)."""
+    arr, n = tiles_array(tiles)
+    L = lib()
+    cnt = int(L.atr_packed_pixel_map(C.cast(arr, C.c_void_p), n, int(width), int(height), None, 0))
+    out = np.zeros(max(cnt, 1), np.int64)
+    L.atr_packed_pixel_map(C.cast(arr, C.c_void_p), n, int(width), int(height), out.ctypes.data, cnt)
+    return out[:cnt]

@@ -1,0 +1,235 @@
+"""Benchmark: Mrays/s of the render path on Dragon 1920x1080 (BASELINE.json metric, config 3).
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--variant auto|lane|wave]
+
+One step = one frame of the config rendered by all ranks: each rank traces its interleaved
+64x64 shard tiles (atr_make_shard_tiles) into a packed buffer; for N > 1 the packed buffers are
+gathered to rank 0 over RCCL (torch.distributed "nccl") and scattered into the frame there.
+The scene (OBJ load, octree build, upload) is prepared before timing; inputs are resident in
+HBM when the timed region starts. value = traced rays of all ranks / max-over-ranks wall time.
+
+Extra JSON fields: roofline (render kernel: algorithmic bytes per launch / average launch time
+from HIP events on the launch stream, against 8 TB/s; traffic = HBM bytes per launch from a
+rocprofv3 --pmc child run, FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes),
+cpu_baseline (the C oracle, i.e. the reference algorithm restated, on the host cores of the
+same box, reference tile scheduler).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 0x853C49E6748FEA9B
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# config -> (asset, W, H, spp, bounces, use_tree)  (BASELINE.json configs)
+CONFIGS = {
+    "c1": ("Cube", 256, 256, 1, 1, True),
+    "c2": ("Monkey", 1280, 720, 1, 1, False),
+    "c3": ("Dragon", 1920, 1080, 1, 1, True),
+    "c4": ("Dragon", 1920, 1080, 64, 5, True),
+    "c5": ("Dragon", 3840, 2160, 256, 5, True),
+}
+GOLDEN_COUNTERS = {"c3": "dragon_1920x1080_tree", "c2": "monkey_1280x720_bf", "c1": "cube_256_tree"}
+
+
+def algorithmic_bytes_per_ray(ctr):
+    """B = 24 (ray) + 12 (hit out) + 28 N_box + 40 N_tri + 8 N_leaf per ray,
+    N_* = the reference's own per-ray work on this input (golden counters, tools/make_goldens.py)."""
+    n = ctr["n_rays"]
+    return (36.0 + 28.0 * ctr["n_box"] / n + 40.0 * ctr["n_tri"] / n + 8.0 * ctr["n_leaf"] / n)
+
+
+def pmc_traffic(args, kernel_name="render_kernel"):
+    """HBM bytes per render launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a
+    short child run of this benchmark. FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950
+    reports half the bytes of wide reads); both counters are in KB."""
+    exe = "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 missing"
+    out = {}
+    for ctr in ["FETCH_SIZE", "WRITE_SIZE"]:
+        d = os.path.join(ROOT, "gpurun_out", f"pmc_{ctr.lower()}")
+        os.makedirs(d, exist_ok=True)
+        cmd = [exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
+               "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+               "--config", args.config, "--variant", args.variant, "--no-cpu-baseline", "--no-pmc"]
+        env = dict(os.environ)
+        env.pop("RANK", None)
+        env.pop("WORLD_SIZE", None)
+        try:
+            subprocess.run(cmd, check=True, timeout=300, env=env, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+        except Exception as e:  # noqa: BLE001
+            return None, f"rocprofv3 {ctr} failed: {e}"
+        vals = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if kernel_name in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                        vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None, f"no {ctr} rows"
+        out[ctr] = sum(vals) / len(vals)
+    return 2.0 * out["FETCH_SIZE"] * 1024.0 + out["WRITE_SIZE"] * 1024.0, "ok"
+
+
+def cpu_baseline(asset, W, H, spp, bounces, use_tree, seconds):
+    """The reference algorithm (C oracle restatement) on this host: reference tile scheduler
+    (renderer.cpp:403-455) on `threads` pthreads, whole frames until `seconds` elapse."""
+    from atray_amd.assets import CENTERS, asset_path
+    from oracle import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    s = O.Scene(asset_path(asset), center=CENTERS[asset], use_tree=use_tree)
+    cam = O.Camera(W, H, spp=spp, bounces=bounces)
+    frames, secs = 0, 0.0
+    while secs < seconds or frames == 0:
+        dt, _, _, _ = s.render_threaded(cam, SEED, threads)
+        secs += dt
+        frames += 1
+    rays = frames * W * H * spp  # traced primary rays; 1 ray per pixel-sample at bounce_limit 1
+    return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} full {asset} {W}x{H} frames spp={spp} bounces={bounces}, "
+                      f"reference tile scheduler ({W // threads}px tiles), {secs:.1f}s of render time"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave"])
+    ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import atray_amd.engine as E
+    from atray_amd.assets import CENTERS, asset_path
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    asset, W, H, spp, bounces, use_tree = CONFIGS[args.config]
+    variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE}[args.variant]
+    mesh = E.Mesh.load_obj(asset_path(asset))
+    box = mesh.translate_to(mesh.aabb(), CENTERS[asset])
+    tree = E.Octree.build(mesh, 300) if use_tree else None
+    eng = E.Engine(local)
+    eng.upload([((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)],
+               [(mesh, tree, box, 1)])
+    cam = E.camera(W, H, spp, bounces)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    all_tiles = [E.make_shard_tiles(W, H, args.side, r, world) for r in range(world)]
+    sizes = [E.packed_size(t) for t in all_tiles]
+    maxn = max(sizes)
+    tiles = E.tiles_array(all_tiles[rank])
+    image = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
+    packed = torch.zeros(maxn, dtype=torch.int32, device=dev)
+    gather = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(world)] if (rank == 0 and world > 1) else None
+    traced = torch.zeros(1, dtype=torch.int64, device=dev)
+    if world == 1:
+        frame = E.atr_frame(E.ATR_LAYOUT_IMAGE, image.data_ptr(), None, None, None, None, None)
+    else:
+        frame = E.atr_frame(E.ATR_LAYOUT_PACKED, packed.data_ptr(), None, None, None, None, None)
+    count_frame = E.atr_frame(frame.layout, frame.framebuffer, None, None, None, None, traced.data_ptr())
+    other_tiles = [E.tiles_array(t) for t in all_tiles]
+
+    def step(fr, evs=None):
+        if evs is not None:
+            evs[0].record()
+        eng.render_start(cam, tiles, fr, SEED, stream=stream, variant=variant)
+        if evs is not None:
+            evs[1].record()
+        if world > 1:
+            dist.gather(packed, gather if rank == 0 else None, dst=0)
+            if rank == 0:
+                for r in range(world):
+                    eng.unpack(other_tiles[r], W, gather[r].data_ptr(), image.data_ptr(), stream)
+
+    # rays per frame (all ranks): counted by the kernel (every get_intersection_data call)
+    step(count_frame)
+    torch.cuda.synchronize()
+    rays_t = traced.clone()
+    if world > 1:
+        dist.all_reduce(rays_t)
+    rays_per_step = int(rays_t.item())
+
+    for _ in range(args.warmup):
+        step(frame)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(frame, evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    rc, _ = eng.wait()
+    assert rc == 0
+
+    if rank == 0:
+        value = rays_per_step * args.steps / elapsed / 1e6
+        out = {"metric": "Mrays/sec on Dragon.obj 1920x1080 @ 1/2/4/8 GPU; % HBM roofline",
+               "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic: the survey's Dragon surrogate (Dragon.obj absent), app camera/materials",
+               "config": {"workload": f"{args.config}: {asset} {W}x{H} spp={spp} bounces={bounces} "
+                                      f"{'octree' if use_tree else 'brute-force'}",
+                          "rays_per_step": rays_per_step, "shard_tile": args.side,
+                          "parallelism": f"tiles{world}", "kernel": args.variant}}
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel_ms": round(kern_ms, 4)}
+        gname = GOLDEN_COUNTERS.get(args.config)
+        if gname:
+            with open(os.path.join(ROOT, "tests", "golden", "goldens.json")) as f:
+                ctr = json.load(f)["hits"][gname]["counters"]
+            bpr = algorithmic_bytes_per_ray(ctr)
+            rays_launch = W * H * spp if world == 1 else sizes[0] * spp
+            achieved = bpr * rays_launch / (kern_ms * 1e-3) / 1e9
+            roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "bytes_per_ray": round(bpr, 1), "rays_per_launch": rays_launch})
+        if world == 1 and not args.no_pmc:
+            traffic, why = pmc_traffic(args)
+            roof["traffic"] = traffic
+            roof["traffic_note"] = why
+        out["roofline"] = roof
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(asset, W, H, spp, bounces, use_tree, args.cpu_seconds)
+            out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

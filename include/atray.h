@@ -1,0 +1,190 @@
+/*
+ * atray.h -- C-ABI of the MI355X (gfx950) intersection engine for ATRay's per-pixel render
+ * loop. Drop-in boundary under the reference's render API (Source/engine/renderer/renderer.h):
+ *
+ *   prep_scene(Scene&, uint32&)                        renderer.h:35 / renderer.cpp:264-291
+ *       -> atr_mesh_load_obj + atr_octree_build (host prerequisites, or the caller's own
+ *          build_KD_tree output flattened by atr_octree_from_nodes) + atr_scene_upload
+ *   start_render_from_camera(RenderInfo&, ThreadPool&) renderer.h:32 / renderer.cpp:403-455
+ *       -> atr_make_tiles + atr_render_start (async on a HIP stream)
+ *   wait_for_render_from_camera_to_finish(...)         renderer.h:33 / renderer.cpp:457-471
+ *       -> atr_render_wait (TRUE/1 = still running, FALSE/0 = done, <0 = error)
+ *
+ * Plain C types and pointers only; every entry point returns an int status (0 = ok,
+ * negative = ATR_E_* or -(1000 + hipError_t)). No exceptions cross the ABI. One context per
+ * GPU; a context is used by one host thread at a time.
+ */
+#ifndef ATRAY_H
+#define ATRAY_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ATR_ABI_VERSION 1
+
+enum {
+    ATR_OK = 0,
+    ATR_E_INVALID = -1,     /* bad argument */
+    ATR_E_IO = -2,          /* file could not be read */
+    ATR_E_NOMEM = -3,
+    ATR_E_NOSCENE = -4,     /* render before atr_scene_upload */
+    ATR_E_TREE_DEPTH = -5,  /* octree deeper than the traversal's mask stack (16 levels) */
+    ATR_E_HIP = -1000       /* -(1000 + hipError_t) */
+};
+
+typedef struct { float x, y, z; } atr_vec3;
+
+/* Material (material.h:4-8). materials[0] is the sky (renderer.cpp:154). */
+typedef struct { atr_vec3 emission, reflection; float scatter; } atr_material;
+
+/* Host mesh = ModelData (model.h:15-23) with 0-based indices (OBJ_loader.cpp:229-267). */
+typedef struct atr_mesh atr_mesh;
+/* Host octree = KD_Tree (kd_tree.h:38-47) flattened in reference node order. */
+typedef struct atr_octree atr_octree;
+
+/* load_model_data (OBJ_loader.h:6): custom parse_f64 (parser.h:113-191), faces keep the first
+   triangle of each polygon, negative indices relative to the end. */
+int atr_mesh_load_obj(const char* path, atr_mesh** out);
+int atr_mesh_parse_obj(const char* text, size_t len, atr_mesh** out);
+/* ModelData from caller arrays (copied). normals may be NULL (flat shading). */
+int atr_mesh_from_arrays(const float* vertices, uint32_t nvertices, const int32_t* face_vertices,
+                         uint32_t nfaces, const float* normals, uint32_t nnormals,
+                         const int32_t* face_normals, atr_mesh** out);
+void atr_mesh_free(atr_mesh* m);
+int atr_mesh_info(const atr_mesh* m, uint32_t* nvertices, uint32_t* nnormals, uint32_t* nfaces);
+/* get_AABB (model.h:41-61): min xyz, max xyz padded by 1e-4. */
+int atr_mesh_aabb(const atr_mesh* m, float aabb_out[6]);
+/* translate_to (model.h:136-152): moves the vertices and the caller's AABB (in/out). */
+int atr_mesh_translate_to(atr_mesh* m, float aabb_inout[6], atr_vec3 new_center);
+
+/* build_KD_tree (kd_tree.cpp:20-64) -> build_oct_kd_tree (:67-288), SAH-named split, leaf
+   size max_faces (app.cpp:77 uses 300). Result is bit-identical to the reference's tree. */
+int atr_octree_build(const atr_mesh* m, uint32_t max_faces, atr_octree** out);
+/* A tree the caller already built (e.g. the reference's own KD_Tree walked into arrays):
+   per node 6 floats (min, max) and children_start_position (0 = leaf); per leaf node its
+   primitive range into prim_vertices (9 floats each) / prim_face. */
+int atr_octree_from_nodes(int32_t nnodes, const float* node_bounds, const int32_t* node_children,
+                          const uint32_t* leaf_first, const uint32_t* leaf_count, uint32_t nprims,
+                          const float* prim_vertices, const uint32_t* prim_face, atr_octree** out);
+void atr_octree_free(atr_octree* t);
+/* Copy the flattened tree out (any pointer may be NULL): 6 floats and children_start_position
+   per node, leaf primitive range per node, 9 floats + face index per leaf primitive. */
+int atr_octree_export(const atr_octree* t, float* node_bounds, int32_t* node_children,
+                      uint32_t* leaf_first, uint32_t* leaf_count, float* prim_vertices,
+                      uint32_t* prim_face);
+/* nodes, inner, leaves, empty leaves, leaf primitive refs, max leaf, depth */
+int atr_octree_stats(const atr_octree* t, int64_t stats_out[7]);
+
+/* Model (model.h:66-71). tree == NULL selects the brute-force branch (renderer.cpp:58-82). */
+typedef struct {
+    const atr_mesh* mesh;
+    const atr_octree* tree;
+    float surrounding_aabb[6];
+    int32_t material;
+} atr_model;
+typedef struct { atr_vec3 center; float radius; int32_t material; } atr_sphere; /* sphere.h:5-10 */
+typedef struct { atr_vec3 normal; float distance; int32_t material; } atr_plane; /* plane.h:5-10 */
+
+/* Camera (camera.h:9-21) + RenderSettings (settings.h:4-10). atr_camera_set = set_camera. */
+typedef struct {
+    int32_t width, height;
+    int32_t anti_aliasing;
+    uint32_t samples_per_pixel;
+    int32_t bounce_limit;
+    float aspect_ratio;
+    atr_vec3 camera_z, camera_x, camera_y, eye, frame_center;
+    float h_fov, half_pixel_width, half_pixel_height;
+} atr_camera;
+int atr_camera_set(atr_camera* cm, atr_vec3 eye, atr_vec3 facing, int32_t width, int32_t height,
+                   int32_t anti_aliasing, uint32_t spp, int32_t bounce_limit, float h_fov);
+
+/* Tile (PL_math.h:147-149,185): inclusive pixel rect, row 0 = bottom. */
+typedef struct { int32_t min_x, min_y, max_x, max_y; } atr_tile;
+/* Reference tile grid (renderer.cpp:406-445): side W/threads (or H/threads), rects overlap by
+   one pixel. Returns the tile count; writes at most cap tiles. */
+int32_t atr_make_tiles(int32_t width, int32_t height, int32_t threads, atr_tile* out, int32_t cap);
+/* Engine tiling for sharding: non-overlapping side x side tiles, tile k owned by rank
+   k % world (interleaved for load balance). Returns the count written for `rank`. */
+int32_t atr_make_shard_tiles(int32_t width, int32_t height, int32_t side, int32_t rank,
+                             int32_t world, atr_tile* out, int32_t cap);
+
+/* ---------------------------------------------------------------- device engine */
+typedef struct atr_ctx atr_ctx;
+int atr_create(int device, atr_ctx** out);
+int atr_destroy(atr_ctx* ctx);
+const char* atr_version(void);
+
+/* Flatten + upload the scene (copies; the caller keeps its buffers). prep_scene's tree build
+   happens before this call (atr_octree_build); upload is not part of the render timing. */
+int atr_scene_upload(atr_ctx* ctx, const atr_material* materials, int32_t nmaterials,
+                     const atr_model* models, int32_t nmodels, const atr_sphere* spheres,
+                     int32_t nspheres, const atr_plane* planes, int32_t nplanes);
+/* device bytes of the uploaded scene, per-model node count and max tree depth */
+int atr_scene_info(atr_ctx* ctx, int64_t* device_bytes, int32_t* max_nodes, int32_t* max_depth);
+
+/* Output layout of a render. IMAGE: pixel (x,y) at y*width + x. PACKED: the pixels of the
+   render's work blocks back to back (atr_render_packed_size); atr_unpack scatters them. */
+enum { ATR_LAYOUT_IMAGE = 0, ATR_LAYOUT_PACKED = 1 };
+
+/* Per-pixel outputs; DEVICE pointers (hipMalloc / torch cuda tensors). Optional ones may be
+   NULL. framebuffer: BGRX u32 (texture.h:27-38). hit_face/hit_t: primary-ray closest hit of
+   sample 0 (face index, 0xFFFFFFFF = miss; t = 3.402823466e38 on miss). rgb: 3 floats per pixel,
+   the spp average before clamp (renderer.cpp:358). ray_casts: the reference's per-pixel
+   non-sky bounce count (renderer.cpp:260). traced_rays: one u64 accumulator (+= every
+   get_intersection_data-equivalent call). */
+typedef struct {
+    int32_t layout;
+    uint32_t* framebuffer;
+    uint32_t* hit_face;
+    float* hit_t;
+    float* rgb;
+    uint32_t* ray_casts;
+    unsigned long long* traced_rays;
+} atr_frame;
+
+/* Kernel variant: AUTO picks the fastest exact variant. All variants are bit-identical. */
+enum { ATR_KERNEL_AUTO = 0, ATR_KERNEL_LANE = 1, ATR_KERNEL_WAVE = 2 };
+
+/* start_render_from_camera: renders the pixels of `tiles` (inclusive rects; overlapping pixels
+   are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the context's own
+   stream). RNG: deterministic per-pixel PCG stream from `seed` (DESIGN.md "RNG"). Returns
+   immediately. */
+int atr_render_start(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                     const atr_frame* frame, uint64_t seed, void* stream);
+/* Like atr_render_start with an explicit kernel variant. */
+int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                        const atr_frame* frame, uint64_t seed, void* stream, int32_t variant);
+/* Number of pixels a PACKED render of these tiles writes. */
+int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles);
+/* Host-only: pixel index (y * width + x) of every slot of a PACKED render of these tiles, in
+   slot order (lets a host consumer read packed buffers). Returns the slot count. */
+int64_t atr_packed_pixel_map(const atr_tile* tiles, int32_t ntiles, int32_t width, int32_t height,
+                             int64_t* out, int64_t cap);
+/* Scatter a PACKED buffer (u32 per pixel) of these tiles into an IMAGE buffer (device). */
+int atr_unpack(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width,
+               const uint32_t* packed, uint32_t* image, void* stream);
+/* Per-tile sum of an IMAGE ray_casts buffer over inclusive (possibly overlapping) tile rects
+   -> the reference's RenderTile::ray_casts (renderer.h:11-15); out is a device int64 array. */
+int atr_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width,
+                       const uint32_t* ray_casts_image, int64_t* out, void* stream);
+/* wait_for_render_from_camera_to_finish: 1 = still running after timeout_ms, 0 = done,
+   <0 = error. tiles_done (optional) = tiles of the last render known complete (progress). */
+int atr_render_wait(atr_ctx* ctx, uint32_t timeout_ms, int32_t* tiles_done);
+
+/* Device-time of the last render's trace kernel(s) in milliseconds (HIP events recorded on the
+   launch stream around the kernel). Valid after atr_render_wait returned 0. */
+int atr_last_kernel_ms(atr_ctx* ctx, float* ms);
+
+/* device memory helpers for C callers without a framework */
+int atr_device_alloc(atr_ctx* ctx, size_t bytes, void** dptr);
+int atr_device_free(atr_ctx* ctx, void* dptr);
+int atr_memcpy_d2h(atr_ctx* ctx, void* dst, const void* src, size_t bytes);
+int atr_memset_d(atr_ctx* ctx, void* dptr, int value, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -258,7 +258,7 @@ int om_build_tree(const om_mesh* m, uint32_t max_faces, om_tree* out) {
     stack[slen++] = 0;
     while (slen > 0) {
         uint32_t ci = stack[--slen];
-        if (T[ci].n > max_faces && depth[ci] < 200) { /* depth guard: reference would not terminate */
+        if (T[ci].n > max_faces && depth[ci] < 64) { /* depth guard: reference would not terminate */
             ov3 sum = v3(0, 0, 0);
             double sum_areas = 0.0;
             for (uint32_t i = 0; i < T[ci].n; i++) { /* :96-104 */

@@ -1,0 +1,110 @@
+"""C-ABI library: loads, exports every symbol include/atray.h declares, and its host-side
+prerequisites (OBJ parse, AABB, translate, octree build, camera, tiles) are bit-identical to
+the oracle. CPU only: no compute call touches a GPU here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from atray_amd import engine as E
+from atray_amd.assets import CENTERS, asset_path
+from oracle import oracle as O
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "atray.h")
+
+
+def header_symbols():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(atr_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = E.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(E.EXPORTS) == syms
+    assert b"gfx950" in L.atr_version()
+
+
+def _engine_tree(asset, leaf=300):
+    m = E.Mesh.load_obj(asset_path(asset))
+    box = m.aabb()
+    box = m.translate_to(box, CENTERS[asset])
+    return m, box, E.Octree.build(m, leaf)
+
+
+@pytest.mark.parametrize("asset", ["Cube", "Monkey", "Deer", "Dragon"])
+def test_octree_bit_identical_to_oracle(asset):
+    m, box, t = _engine_tree(asset)
+    s = O.Scene(asset_path(asset), center=CENTERS[asset])
+    assert np.array_equal(box.view(np.uint32), s.surrounding_aabb.view(np.uint32))
+    st = t.stats()
+    os_ = s.tree_stats()
+    for k in ["nodes", "inner", "leaves", "empty_leaves", "leaf_prim_refs", "max_leaf"]:
+        assert st[k] == os_[k], k
+    assert st["depth"] < 16
+    bounds, children, first, count, verts, face = t.export()
+    nodes, otri, oface = s.tree_arrays()
+    assert np.array_equal(bounds[:, :3].view(np.uint32), nodes["bmin"].view(np.uint32))
+    assert np.array_equal(bounds[:, 3:].view(np.uint32), nodes["bmax"].view(np.uint32))
+    assert np.array_equal(children, nodes["children"])
+    leaf = children == 0
+    assert np.array_equal(first[leaf], nodes["prim_off"][leaf])
+    assert np.array_equal(count[leaf], nodes["prim_cnt"][leaf])
+    assert np.array_equal(verts.view(np.uint32), otri.view(np.uint32))
+    assert np.array_equal(face, oface)
+
+
+def test_octree_from_nodes_roundtrip():
+    s = O.Scene(asset_path("Monkey"), center=CENTERS["Monkey"])
+    nodes, tri, face = s.tree_arrays()
+    bounds = np.concatenate([nodes["bmin"], nodes["bmax"]], 1)
+    t = E.Octree.from_nodes(bounds, nodes["children"], nodes["prim_off"], nodes["prim_cnt"], tri, face)
+    assert t.stats()["nodes"] == len(nodes)
+    with pytest.raises(E.AtrError):  # leaf range past the primitive array
+        bad = nodes["prim_cnt"].copy()
+        bad[nodes["children"] == 0] += 10**6
+        E.Octree.from_nodes(bounds, nodes["children"], nodes["prim_off"], bad, tri, face)
+
+
+def test_mesh_parser_matches_oracle_on_quirky_text():
+    txt = ("# c\nv 0.1 0.2 0.3\nv 1e1 -2.5E-1 +3\nv 1 1 1\nv 2 2 2\nvt 0.5 0.5\nvn 0 0 1\n"
+           "f 1/1/1 2/1/1 3/1/1 4/1/1\nf -4//1 -3//1 -2//1\nusemtl x\nf 1 2 3")
+    m = E.Mesh.parse_obj(txt)
+    assert m.info() == (4, 1, 3)
+    s = O.Scene(obj_text=txt, center=None, use_tree=False)
+    V, N, FV, FN = s.mesh_arrays()
+    assert np.array_equal(m.aabb().view(np.uint32), s.surrounding_aabb.view(np.uint32))
+
+
+def test_camera_matches_oracle():
+    for (w, h, aa, spp, b) in [(1920, 1080, 0, 1, 1), (256, 256, 1, 4, 5), (7, 3, 0, 2, 2)]:
+        ce = E.camera(w, h, spp, b, aa)
+        co = O.Camera(w, h, spp=spp, bounces=b, aa=aa).c
+        assert bytes(ce) == bytes(co)
+
+
+@pytest.mark.parametrize("wht", [(1280, 720, 8), (1920, 1080, 8), (256, 256, 1), (100, 30, 8), (5, 5, 8)])
+def test_reference_tiles_match_oracle(wht):
+    w, h, t = wht
+    assert np.array_equal(E.make_tiles(w, h, t), O.make_tiles(w, h, t))
+
+
+def test_shard_tiles_partition_the_image():
+    W, H = 1920, 1080
+    cover = np.zeros((H, W), np.int32)
+    for r in range(3):
+        for x0, y0, x1, y1 in E.make_shard_tiles(W, H, 64, r, 3):
+            cover[y0:y1 + 1, x0:x1 + 1] += 1
+    assert (cover == 1).all()
+
+
+def test_packed_size_counts_union_of_overlapping_tiles():
+    tiles = E.make_tiles(1280, 720, 8)  # inclusive tiles overlapping by one pixel
+    assert E.packed_size(tiles) == 1280 * 720
+    assert E.packed_size([[0, 0, 9, 9], [5, 5, 14, 14]]) == 100 + 100 - 25
