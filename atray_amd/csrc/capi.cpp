@@ -438,6 +438,27 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
             }
             std::vector<DTri> tris(T.prim_face.size());
             for (size_t k = 0; k < tris.size(); ++k) tris[k] = make_tri(&T.prim_vertices[9 * k], T.prim_face[k]);
+            {
+                const size_t np = tris.size() ? tris.size() : 1;
+                std::vector<float4_t> s0(np), s1(np);
+                std::vector<float> s2(np, 0.f);
+                std::vector<uint32_t> sf(np, 0u);
+                for (size_t k = 0; k < tris.size(); ++k) {
+                    const DTri& t = tris[k];
+                    s0[k] = float4_t{t.ax, t.ay, t.az, t.abx};
+                    s1[k] = float4_t{t.aby, t.abz, t.acx, t.acy};
+                    s2[k] = t.acz;
+                    sf[k] = t.face;
+                }
+                if ((rc = dev_upload(c, s0.data(), s0.size() * sizeof(float4_t), &p))) return rc;
+                dm.t0 = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
+                dm.t1 = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, s2.data(), s2.size() * sizeof(float), &p))) return rc;
+                dm.t2 = static_cast<const float*>(p);
+                if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
+                dm.tface = static_cast<const uint32_t*>(p);
+            }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
             dm.nodes = static_cast<const DNode*>(p);
             if ((rc = dev_upload(c, range.data(), range.size() * sizeof(uint32_t), &p))) return rc;
@@ -536,7 +557,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     if (fr->layout != ATR_LAYOUT_IMAGE && fr->layout != ATR_LAYOUT_PACKED) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
     int rc = ATR_OK;
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
@@ -555,7 +576,9 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.ray_casts = fr->ray_casts;
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
-    const int wave = variant == ATR_KERNEL_LANE ? 0 : 1;  // AUTO -> WAVE
+    P.counters = nullptr;
+    // AUTO -> LANE (measured fastest); 16 + n = LANE at n waves/SIMD (diagnostic)
+    const int wave = variant >= 16 ? variant : (variant == ATR_KERNEL_WAVE ? 1 : 0);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(atr_launch_render(P, wave, s));
     HIPCHK(hipEventRecord(c->ev_stop, s));
@@ -563,6 +586,40 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     c->have_render = true;
     c->last_stream = s;
     c->last_ntiles = ntiles;
+    return ATR_OK;
+}
+
+int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                        uint64_t seed, int32_t variant, int64_t out[8]) {
+    if (!c || !cam || !out || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
+    if (!bs) return rc;
+    void* fb = nullptr;
+    void* ctr = nullptr;
+    HIPCHK(hipMalloc(&fb, size_t(cam->width) * size_t(cam->height) * 4));
+    HIPCHK(hipMalloc(&ctr, 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctr, 0, 8 * sizeof(unsigned long long)));
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.blocks = static_cast<const DBlock*>(bs->dev.p);
+    P.nblocks = int32_t(bs->host.size());
+    P.layout = ATR_LAYOUT_IMAGE;
+    P.framebuffer = static_cast<uint32_t*>(fb);
+    P.error_flag = c->d_error;
+    P.counters = static_cast<unsigned long long*>(ctr);
+    HIPCHK(atr_launch_render(P, variant == ATR_KERNEL_WAVE ? 1 : 0, nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long h[8];
+    HIPCHK(hipMemcpy(h, ctr, sizeof(h), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 8; ++k) out[k] = int64_t(h[k]);
+    HIPCHK(hipFree(fb));
+    HIPCHK(hipFree(ctr));
     return ATR_OK;
 }
 
@@ -611,7 +668,7 @@ int atr_unpack(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width,
     int rc = ATR_OK;
     BlockSet* bs = get_blocks(c, tiles, ntiles, width, H, rc);
     if (!bs) return rc;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
     HIPCHK(atr_launch_unpack(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed, image, s));
     return ATR_OK;
 }
@@ -620,7 +677,7 @@ int atr_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_
                        const uint32_t* casts, int64_t* out, void* stream) {
     if (!c || !casts || !out || width <= 0 || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
     void* dt = nullptr;
     HIPCHK(hipMallocAsync(&dt, sizeof(atr_tile) * size_t(ntiles ? ntiles : 1), s));
     HIPCHK(hipMemcpyAsync(dt, tiles, sizeof(atr_tile) * size_t(ntiles), hipMemcpyHostToDevice, s));

@@ -16,6 +16,8 @@
 
 namespace atr {
 
+struct alignas(16) float4_t { float x, y, z, w; };
+
 constexpr float kMaxFloat = 3.402823466e+38F;     // PL_base_defs.h:72
 constexpr float kInvU32Max = 2.328306437e-10F;    // PL_base_defs.h:75
 constexpr float kTol = 0.0001f;                   // ray.h:5
@@ -90,6 +92,12 @@ struct DModel {
     const DNode* nodes;          // octree nodes in reference order (root = 0)
     const uint32_t* leaf_range;  // 2 u32 per node: first DTri, count (leaves only)
     const DTri* tris;            // leaf-ordered primitives (tree) or face-ordered (brute force)
+    // the same primitives as SoA streams for per-lane loads: t0 = {a.xyz, ab.x},
+    // t1 = {ab.yz, ac.xy}, t2 = ac.z (36 B per test); tface read only for the final hit
+    const float4_t* t0;
+    const float4_t* t1;
+    const float* t2;
+    const uint32_t* tface;
     const float* shade;          // 9 f32 per face: smooth -> na, nb, nc; flat -> v0, v1, v2
     uint32_t nfaces;
     int32_t has_tree;
@@ -137,6 +145,7 @@ struct RenderParams {
     uint32_t* ray_casts;
     unsigned long long* traced_rays;
     int32_t* error_flag;  // set to 1 if a ray hit a traversal limit (never for depth <= 16)
+    unsigned long long* counters;  // non-null -> instrumented kernel (8 u64, see render.hip)
 };
 
 }  // namespace atr

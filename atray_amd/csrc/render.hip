@@ -28,31 +28,99 @@ struct Isect {
 constexpr int kLeafBuf = 8;
 
 // ------------------------------------------------------------------ LANE schedule
-__device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m, Hit& h, int& err) {
+// Per-lane leaf scan over the SoA triangle streams, one triangle of prefetch: the loads of
+// triangle k+1 are in flight while triangle k is tested. The hit keeps the primitive SLOT;
+// its face index is read once, after the tree query.
+struct TriRegs { float4_t q0, q1; float q2; };
+
+__device__ __forceinline__ void tri_fetch(const DModel& m, uint32_t i, TriRegs& t) {
+    t.q0 = m.t0[i];
+    t.q1 = m.t1[i];
+    t.q2 = m.t2[i];
+}
+
+__device__ __forceinline__ void tri_test(const Ray& r, const TriRegs& t, uint32_t slot, float& best_t,
+                                         uint32_t& best_slot, float& bu, float& bv, bool& improved) {
+    float u = 0.f, v = 0.f;
+    const float dist = tri_hit(r, mk(t.q0.x, t.q0.y, t.q0.z), mk(t.q0.w, t.q1.x, t.q1.y),
+                               mk(t.q1.z, t.q1.w, t.q2), u, v);
+    if (dist < best_t && dist > kTol) {
+        best_t = dist;
+        best_slot = slot;
+        bu = u;
+        bv = v;
+        improved = true;
+    }
+}
+
+// Per-lane leaf scan over the SoA triangle streams, software-pipelined two deep with two
+// register sets used alternately (no copies, so the loads of the next triangle stay in
+// flight while the current one is tested). The hit keeps the primitive SLOT; its face index
+// is read once, after the tree query.
+template <bool COUNT>
+__device__ __forceinline__ bool scan_leaf_lane(const Ray& r, const DModel& m, uint32_t first,
+                                               uint32_t count, float& best_t, uint32_t& best_slot,
+                                               float& bu, float& bv, Ctr& ct) {
+    if constexpr (COUNT) { ct.tri += count; ct.leaf += 1; }
+    bool improved = false;
+    if (count == 0) return false;
+    const uint32_t end = first + count;
+    TriRegs A, B;
+    tri_fetch(m, first, A);
+    for (uint32_t k = first; k < end; k += 2) {
+        const bool has_b = k + 1 < end;
+        if (has_b) tri_fetch(m, k + 1, B);
+        tri_test(r, A, k, best_t, best_slot, bu, bv, improved);
+        if (k + 2 < end) tri_fetch(m, k + 2, A);
+        if (has_b) tri_test(r, B, k + 1, best_t, best_slot, bu, bv, improved);
+    }
+    return improved;
+}
+
+// Sorted-leaf scan with a rotating head: entry 0 is always the next leaf, the buffer shifts
+// down after each scanned leaf (static register moves, no dynamically indexed arrays).
+template <int K>
+__device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
+#pragma unroll
+    for (int j = 0; j + 1 < K; ++j) { b.d[j] = b.d[j + 1]; b.node[j] = b.node[j + 1]; b.idx[j] = b.idx[j + 1]; }
+    b.d[K - 1] = __builtin_inff();
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m, Hit& h, int& err, Ctr& ct) {
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
     const NodeBox root = load_node(m.nodes, 0);
+    if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
     if (!box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) return;  // :339
+    uint32_t slot = 0xFFFFFFFFu;
     if (root.children == 0) {  // :344-361
-        scan_leaf(r, m.tris, m.leaf_range[0], m.leaf_range[1], h);
-        return;
-    }
-    float bd = -__builtin_inff();
-    int32_t bi = -1;
-    for (;;) {
-        LeafBuf<kLeafBuf> lb;
-        const int32_t n = traverse_pass<kLeafBuf>(r, m.nodes, lb, bd, bi);
-        if (n < 0) { err = 1; return; }
-        const int32_t nb = n < kLeafBuf ? n : kLeafBuf;
-        for (int32_t j = 0; j < nb; ++j) {
-            const int32_t leaf = lb_node<kLeafBuf>(lb, j);
-            if (scan_leaf(r, m.tris, m.leaf_range[2 * leaf], m.leaf_range[2 * leaf + 1], h)) return;
+        scan_leaf_lane<COUNT>(r, m, m.leaf_range[0], m.leaf_range[1], h.t, slot, h.u, h.v, ct);
+    } else {
+        float bd = -__builtin_inff();
+        int32_t bi = -1;
+        bool more = true;
+        while (more) {
+            LeafBuf<kLeafBuf> lb;
+            const int32_t n = traverse_pass<kLeafBuf, COUNT>(r, m.nodes, lb, bd, bi, ct);
+            if (n < 0) { err = 1; break; }
+            int32_t nb = n < kLeafBuf ? n : kLeafBuf;
+            more = n > kLeafBuf;
+            bool hit = false;
+            while (nb > 0) {
+                const int32_t leaf = lb.node[0];
+                bd = lb.d[0];
+                bi = lb.idx[0];
+                if (scan_leaf_lane<COUNT>(r, m, m.leaf_range[2 * leaf], m.leaf_range[2 * leaf + 1], h.t, slot,
+                                          h.u, h.v, ct)) { hit = true; break; }
+                lb_pop<kLeafBuf>(lb);
+                --nb;
+            }
+            if (hit) break;
         }
-        if (n <= kLeafBuf) return;
-        bd = lb.d[kLeafBuf - 1];
-        bi = lb.idx[kLeafBuf - 1];
     }
+    if (slot != 0xFFFFFFFFu) h.face = m.tface[slot];
 }
 
 // ------------------------------------------------------------------ WAVE schedule
@@ -66,11 +134,12 @@ struct TreeQuery {
     int32_t state;   // 0 = needs a pass, 1 = has leaves in buffer, 2 = done
 };
 
-__device__ __forceinline__ int32_t tq_next_leaf(TreeQuery& q, const Ray& r, const DModel& m, int& err) {
+template <bool COUNT>
+__device__ __forceinline__ int32_t tq_next_leaf(TreeQuery& q, const Ray& r, const DModel& m, int& err, Ctr& ct) {
     for (;;) {
         if (q.state == 2) return -1;
         if (q.state == 0) {
-            q.ncand = traverse_pass<kLeafBuf>(r, m.nodes, q.lb, q.bd, q.bi);
+            q.ncand = traverse_pass<kLeafBuf, COUNT>(r, m.nodes, q.lb, q.bd, q.bi, ct);
             if (q.ncand < 0) { err = 1; q.state = 2; return -1; }
             q.pos = 0;
             q.state = 1;
@@ -86,9 +155,11 @@ __device__ __forceinline__ int32_t tq_next_leaf(TreeQuery& q, const Ray& r, cons
 
 // Scan a wave-uniform leaf: every operand address is uniform, so the triangle records are
 // fetched by the scalar unit once per wavefront instead of once per lane.
+template <bool COUNT>
 __device__ __forceinline__ bool scan_leaf_uniform(const Ray& r, const DTri* __restrict__ tris,
-                                                  uint32_t first, uint32_t count, Hit& h) {
+                                                  uint32_t first, uint32_t count, Hit& h, Ctr& ct) {
     bool improved = false;
+    if constexpr (COUNT) { ct.tri += count; ct.leaf += 1; }
     for (uint32_t k = 0; k < count; ++k) {
         const DTri* t = tris + first + k;  // uniform address -> s_load_dwordx8 + s_load_dwordx2
         const V3 a = mk(t->ax, t->ay, t->az);
@@ -107,8 +178,9 @@ __device__ __forceinline__ bool scan_leaf_uniform(const Ray& r, const DTri* __re
     return improved;
 }
 
+template <bool COUNT>
 __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m, bool active, Hit& h,
-                                                  int& err) {
+                                                  int& err, Ctr& ct) {
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
@@ -117,33 +189,35 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
     int32_t root_leaf_scan = 0;
     if (active) {
         const NodeBox root = load_node(m.nodes, 0);
+        if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
         if (box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) {
             if (root.children == 0) root_leaf_scan = 1;
             else { q.bd = -__builtin_inff(); q.bi = -1; q.state = 0; }
         }
     }
     int32_t leaf = -1;
-    if (q.state != 2) leaf = tq_next_leaf(q, r, m, err);
+    if (q.state != 2) leaf = tq_next_leaf<COUNT>(q, r, m, err, ct);
     if (root_leaf_scan) leaf = 0;
     for (;;) {
         const uint64_t want = __ballot(leaf >= 0);
         if (want == 0) break;
         const int src = __builtin_ctzll(want);
         const int32_t L = __builtin_amdgcn_readlane(leaf, src);  // uniform
+        if constexpr (COUNT) ct.wave_tri += m.leaf_range[2 * L + 1];  // every lane: wave-level count
         if (leaf == L) {
             const uint32_t first = m.leaf_range[2 * L], count = m.leaf_range[2 * L + 1];
-            const bool hit = scan_leaf_uniform(r, m.tris, __builtin_amdgcn_readfirstlane(first),
-                                               __builtin_amdgcn_readfirstlane(count), h);
+            const bool hit = scan_leaf_uniform<COUNT>(r, m.tris, __builtin_amdgcn_readfirstlane(first),
+                                                      __builtin_amdgcn_readfirstlane(count), h, ct);
             if (root_leaf_scan || hit) { q.state = 2; leaf = -1; }
-            else { ++q.pos; leaf = tq_next_leaf(q, r, m, err); }
+            else { ++q.pos; leaf = tq_next_leaf<COUNT>(q, r, m, err, ct); }
         }
     }
 }
 
 // ------------------------------------------------------------------ get_intersection_data
-template <bool WAVE>
+template <bool WAVE, bool COUNT>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
-                                                Isect& id, int& err) {
+                                                Isect& id, int& err, Ctr& ct) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
     float best = kMaxFloat;
     int32_t nm = -1, ns = -1, np = -1;
@@ -154,12 +228,14 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
         const DModel& m = S->models[i];
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
             Hit h;
-            if (WAVE) tree_closest_wave(r, m, active, h, err);
-            else if (active) tree_closest_lane(r, m, h, err);
+            if (WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
+            else if (active) tree_closest_lane<COUNT>(r, m, h, err, ct);
             else h.t = kMaxFloat;
             if (h.t > kTol && h.t < best) { best = h.t; face = h.face; fu = h.u; fv = h.v; nm = i; }
         } else if (active) {  // brute force (:58-82), face-ordered triangles, uniform loads
+            if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
             if (box_entry(r, m.aabb[0], m.aabb[1], m.aabb[2], m.aabb[3], m.aabb[4], m.aabb[5]) != 0) {
+                if constexpr (COUNT) { ct.tri += m.nfaces; }
                 for (uint32_t j = 0; j < m.nfaces; ++j) {
                     const DTri* t = m.tris + j;
                     float u = 0.f, v = 0.f;
@@ -230,11 +306,11 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
 }
 
 // ------------------------------------------------------------------ cast_ray + pixel loop
-template <bool WAVE>
+template <bool WAVE, bool COUNT>
 __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d, int32_t bounce_limit,
                                        bool active, uint64_t& st, uint64_t stream, uint32_t& casts,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
-                                       int& err) {
+                                       int& err, Ctr& ct) {
     V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
     int32_t i = 0;
     bool live = active;
@@ -246,7 +322,7 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
         else if (!go) break;
         Isect id;
         id.type = T_NONE;
-        intersect_scene<WAVE>(S, o, d, go, id, err);
+        intersect_scene<WAVE, COUNT>(S, o, d, go, id, err, ct);
         if (!go) continue;
         ++traced;
         if (record && i == 0) { hit_face = id.face; hit_t = id.t; }
@@ -283,8 +359,13 @@ __device__ __forceinline__ int remap_xcd(int wg, int nwg) {
     return (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + wg / 8;
 }
 
-template <bool WAVE>
-__global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
+// PRIMARY: bounce_limit == 1 and no AA. Then cast_ray is one intersection whose color is the
+// hit material's (or the sky's) emission; the three rand_bi draws and the bounce ray it builds
+// feed only a second iteration that never runs (renderer.cpp:222-259), so they are skipped --
+// output bit-identical, and far fewer live registers. Every sample re-traces the same primary
+// ray in the reference (:353-356) and sums the same color, reproduced by the same f32 adds.
+template <bool WAVE, bool COUNT, bool PRIMARY, int OCC = 4>
+__global__ __launch_bounds__(256, OCC) void render_kernel(RenderParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = remap_xcd(blockIdx.x, gridDim.x) * 4 + wave;
     if (b >= P.nblocks) return;  // whole wavefront
@@ -295,6 +376,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     const atr_camera& cm = P.cam;
     const DScene* S = P.scene;
     int err = 0;
+    Ctr ct;
     uint32_t casts = 0, traced = 0, hit_face = 0xFFFFFFFFu;
     float hit_t = kMaxFloat;
     V3 col = mk(0.f, 0.f, 0.f);
@@ -305,14 +387,31 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     const V3 eye = from(cm.eye), fc = from(cm.frame_center), cx = from(cm.camera_x), cy = from(cm.camera_y);
     V3 dir = mk(0.f, 0.f, 1.f);
     if (!cm.anti_aliasing) dir = unit(sub(add(add(fc, scale(cx, film_x)), scale(cy, film_y)), eye));  // :350-351
+    if constexpr (PRIMARY) {
+        Isect id;
+        id.type = T_NONE;
+        intersect_scene<WAVE, COUNT>(S, eye, dir, active, id, err, ct);
+        if (active) {
+            const DMaterial& mat = S->mats[id.material];
+            const V3 ret = mk(mat.ex, mat.ey, mat.ez);  // weight (1,1,1) x emission
+            hit_face = id.face;
+            hit_t = id.t;
+            const uint32_t hit = id.type == T_SKY ? 0u : 1u;
+            for (uint32_t s = 0; s < cm.samples_per_pixel; ++s) {
+                col = add(col, ret);
+                casts += hit;
+                ++traced;
+            }
+        }
+    } else
     for (uint32_t s = 0; s < cm.samples_per_pixel; ++s) {
         if (cm.anti_aliasing) {  // :338-343
             const float xo = rand_bi(st, stream) * cm.half_pixel_width + film_x;
             const float yo = rand_bi(st, stream) * cm.half_pixel_height + film_y;
             dir = unit(sub(add(add(fc, scale(cx, xo)), scale(cy, yo)), eye));
         }
-        col = add(col, cast_ray<WAVE>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
-                                      s == 0, hit_face, hit_t, err));
+        col = add(col, cast_ray<WAVE, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
+                                             s == 0, hit_face, hit_t, err, ct));
     }
     if (active) {
         col = divs(col, float(cm.samples_per_pixel));  // :358
@@ -337,10 +436,32 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
         if (lane == 0 && t) atomicAdd(P.traced_rays, (unsigned long long)t);
     }
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
+    if constexpr (COUNT) {
+        // counters[0..7]: rays, box(ref), tri, leaf, wave_tri_iters, passes, box_all, waves
+        uint32_t v[6] = {ct.box, ct.tri, ct.leaf, ct.wave_tri, ct.pass, ct.box_all};
+        unsigned long long* C = P.counters;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            uint32_t t = v[k];
+            if (k == 3) t = (lane == 0) ? t : 0u;  // wave-level count: every lane holds the same value
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+            if (lane == 0 && t) atomicAdd(C + 1 + k, (unsigned long long)t);
+        }
+        uint32_t t = traced;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if (lane == 0) { atomicAdd(C + 0, (unsigned long long)t); atomicAdd(C + 7, 1ull); }
+    }
 }
 
-template __global__ void render_kernel<false>(RenderParams);
-template __global__ void render_kernel<true>(RenderParams);
+#define ATR_INST(W, C, PR) template __global__ void render_kernel<W, C, PR>(RenderParams);
+ATR_INST(false, false, false) ATR_INST(true, false, false) ATR_INST(false, true, false) ATR_INST(true, true, false)
+ATR_INST(false, false, true) ATR_INST(true, false, true) ATR_INST(false, true, true) ATR_INST(true, true, true)
+#undef ATR_INST
+template __global__ void render_kernel<false, false, true, 5>(RenderParams);
+template __global__ void render_kernel<false, false, true, 6>(RenderParams);
+template __global__ void render_kernel<false, false, true, 8>(RenderParams);
 
 __global__ __launch_bounds__(256) void unpack_kernel(const DBlock* __restrict__ blocks, int32_t nblocks,
                                                      int32_t width, const uint32_t* __restrict__ packed,
@@ -377,11 +498,34 @@ __global__ __launch_bounds__(256) void tile_casts_kernel(const atr_tile* __restr
 }  // namespace atr
 
 // launchers used by capi.cpp
+// Default occupancy of the PRIMARY lane kernel (waves/SIMD; chosen by measurement).
+constexpr int kPrimaryOcc = 5;
+
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s) {
     const int grid = (P.nblocks + 3) / 4;
     if (grid <= 0) return hipSuccess;
-    if (wave) hipLaunchKernelGGL(atr::render_kernel<true>, dim3(grid), dim3(256), 0, s, P);
-    else hipLaunchKernelGGL(atr::render_kernel<false>, dim3(grid), dim3(256), 0, s, P);
+    const int occ = wave >= 16 ? wave - 16 : (wave ? 0 : kPrimaryOcc);  // 16+occ: explicit occupancy
+    if (wave >= 16) wave = 0;
+    const bool count = P.counters != nullptr;
+    const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
+    const int key = (wave ? 4 : 0) | (count ? 2 : 0) | (prim ? 1 : 0);
+    const dim3 g(grid), b(256);
+    if (key == 1 && occ != 4) {
+        if (occ == 5) hipLaunchKernelGGL((atr::render_kernel<false, false, true, 5>), g, b, 0, s, P);
+        else if (occ == 6) hipLaunchKernelGGL((atr::render_kernel<false, false, true, 6>), g, b, 0, s, P);
+        else hipLaunchKernelGGL((atr::render_kernel<false, false, true, 8>), g, b, 0, s, P);
+        return hipGetLastError();
+    }
+    switch (key) {
+        case 0: hipLaunchKernelGGL((atr::render_kernel<false, false, false>), g, b, 0, s, P); break;
+        case 1: hipLaunchKernelGGL((atr::render_kernel<false, false, true>), g, b, 0, s, P); break;
+        case 2: hipLaunchKernelGGL((atr::render_kernel<false, true, false>), g, b, 0, s, P); break;
+        case 3: hipLaunchKernelGGL((atr::render_kernel<false, true, true>), g, b, 0, s, P); break;
+        case 4: hipLaunchKernelGGL((atr::render_kernel<true, false, false>), g, b, 0, s, P); break;
+        case 5: hipLaunchKernelGGL((atr::render_kernel<true, false, true>), g, b, 0, s, P); break;
+        case 6: hipLaunchKernelGGL((atr::render_kernel<true, true, false>), g, b, 0, s, P); break;
+        default: hipLaunchKernelGGL((atr::render_kernel<true, true, true>), g, b, 0, s, P); break;
+    }
     return hipGetLastError();
 }
 

@@ -15,6 +15,13 @@
 
 namespace atr {
 
+// Diagnostic work counters (compiled out unless a COUNT kernel is built): the reference-
+// equivalent work (box tests of the first DFS pass + root, triangle tests, leaves scanned) and
+// the engine's own extra work (re-walk passes, all box tests, wave-level triangle iterations).
+struct Ctr {
+    uint32_t box = 0, box_all = 0, tri = 0, leaf = 0, wave_tri = 0, pass = 0;
+};
+
 struct Ray {
     V3 o, d, inv;
     int s0, s1, s2;  // inv_signs (renderer.cpp:41-44)
@@ -115,8 +122,10 @@ struct Hit {
 };
 
 // Scan one leaf's primitives in leaf order (kd_tree.cpp:440-456). True if `h` improved.
+template <bool COUNT>
 __device__ __forceinline__ bool scan_leaf(const Ray& r, const DTri* __restrict__ tris, uint32_t first,
-                                          uint32_t count, Hit& h) {
+                                          uint32_t count, Hit& h, Ctr& ct) {
+    if constexpr (COUNT) { ct.tri += count; ct.leaf += 1; }
     bool improved = false;
     for (uint32_t k = 0; k < count; ++k) {
         const TriRec t = load_tri(tris, first + k);
@@ -175,14 +184,16 @@ __device__ __forceinline__ int32_t lb_node(const LeafBuf<K>& b, int j) {
 
 // Examine the children of an inner node (kd_tree.cpp:370-434): box-test children in order
 // until 5 have been hit; inner hits -> returned bit mask, leaf hits -> leaf order buffer.
-template <int K>
+template <int K, bool COUNT>
 __device__ __forceinline__ uint32_t examine_children(const Ray& r, const DNode* __restrict__ nodes,
                                                      int32_t first, LeafBuf<K>& lb, int32_t& disc,
-                                                     int32_t& ncand, float bd, int32_t bi) {
+                                                     int32_t& ncand, float bd, int32_t bi, Ctr& ct,
+                                                     bool first_pass) {
     uint32_t mask = 0;
     int nodes_hit = 0;
     for (int i = 0; i < 8 && nodes_hit <= 4; ++i) {
         const NodeBox c = load_node(nodes, first + i);
+        if constexpr (COUNT) { ct.box_all += 1; ct.box += first_pass ? 1u : 0u; }
         if (c.children != 0) {
             if (box_check(r, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz)) {
                 ++nodes_hit;
@@ -206,13 +217,15 @@ __device__ __forceinline__ uint32_t examine_children(const Ray& r, const DNode* 
 // One DFS pass over the inner nodes (the reference's hit-stack loop, kd_tree.cpp:363-435),
 // keeping the K first leaves (in sorted order) strictly after (bd, bi). Returns the number of
 // candidate leaves after the bound, or -1 if the tree is deeper than the mask stack.
-template <int K>
+template <int K, bool COUNT>
 __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const DNode* __restrict__ nodes,
-                                                 LeafBuf<K>& lb, float bd, int32_t bi) {
+                                                 LeafBuf<K>& lb, float bd, int32_t bi, Ctr& ct) {
+    const bool first_pass = bi < 0;
+    if constexpr (COUNT) ct.pass += 1;
     lb_clear<K>(lb);
     int32_t disc = 0, ncand = 0;
     const NodeBox root = load_node(nodes, 0);
-    uint64_t lo = examine_children<K>(r, nodes, root.children, lb, disc, ncand, bd, bi);
+    uint64_t lo = examine_children<K, COUNT>(r, nodes, root.children, lb, disc, ncand, bd, bi, ct, first_pass);
     uint64_t hi = 0;
     int32_t p = 0, pfirst = root.children, lvl = 0;
     for (;;) {
@@ -223,7 +236,7 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const DNode* __re
             else hi &= ~(uint64_t(1) << (8 * (lvl - 8) + s));
             const int32_t c = pfirst + s;
             const NodeBox cn = load_node(nodes, c);
-            const uint64_t cm = examine_children<K>(r, nodes, cn.children, lb, disc, ncand, bd, bi);
+            const uint64_t cm = examine_children<K, COUNT>(r, nodes, cn.children, lb, disc, ncand, bd, bi, ct, first_pass);
             ++lvl;
             if (lvl >= kMaskLevels) return -1;
             if (lvl < 8) lo |= cm << (8 * lvl);

@@ -86,6 +86,7 @@ EXPORTS = [
     "atr_octree_from_nodes", "atr_octree_free", "atr_octree_export", "atr_octree_stats", "atr_camera_set",
     "atr_make_tiles", "atr_make_shard_tiles", "atr_create", "atr_destroy", "atr_version",
     "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
+    "atr_render_counters",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d",
@@ -129,6 +130,7 @@ def lib():
         "atr_render_start": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp], C.c_int),
         "atr_render_start_ex": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32], C.c_int),
         "atr_render_packed_size": ([vp, i32], i64),
+        "atr_render_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, i64 * 8], C.c_int),
         "atr_packed_pixel_map": ([vp, i32, i32, i32, vp, i64], i64),
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
@@ -319,6 +321,14 @@ class Engine:
                                         C.byref(frame), C.c_uint64(seed & (2**64 - 1)),
                                         C.c_void_p(stream) if stream else None, int(variant)),
               "render start")
+
+    def counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        out = (C.c_int64 * 8)()
+        check(lib().atr_render_counters(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n,
+                                        C.c_uint64(seed & (2**64 - 1)), int(variant), out), "counters")
+        keys = ["n_rays", "n_box", "n_tri", "n_leaf", "wave_tri_iters", "passes", "box_all", "waves"]
+        return dict(zip(keys, [int(x) for x in out]))
 
     def wait(self, timeout_ms=0xFFFFFFFF):
         done = C.c_int32()

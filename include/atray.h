@@ -149,14 +149,19 @@ typedef struct {
 enum { ATR_KERNEL_AUTO = 0, ATR_KERNEL_LANE = 1, ATR_KERNEL_WAVE = 2 };
 
 /* start_render_from_camera: renders the pixels of `tiles` (inclusive rects; overlapping pixels
-   are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the context's own
-   stream). RNG: deterministic per-pixel PCG stream from `seed` (DESIGN.md "RNG"). Returns
+   are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the null stream, HIP's convention). RNG: deterministic per-pixel PCG stream from `seed` (DESIGN.md "RNG"). Returns
    immediately. */
 int atr_render_start(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                      const atr_frame* frame, uint64_t seed, void* stream);
 /* Like atr_render_start with an explicit kernel variant. */
 int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         const atr_frame* frame, uint64_t seed, void* stream, int32_t variant);
+/* Diagnostic, synchronous: an instrumented render of the same work that returns
+   [0] traced rays, [1] box tests, [2] triangle tests, [3] leaves scanned -- the reference's own
+   per-ray work on this input (kd_tree.cpp:337-465) -- and the engine's [4] wave-level triangle
+   iterations, [5] DFS passes, [6] all box tests, [7] wavefronts. */
+int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                        uint64_t seed, int32_t variant, int64_t counters_out[8]);
 /* Number of pixels a PACKED render of these tiles writes. */
 int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles);
 /* Host-only: pixel index (y * width + x) of every slot of a PACKED render of these tiles, in

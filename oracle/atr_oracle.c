@@ -416,6 +416,8 @@ static inline float mt_culled(ov3 o, ov3 d, ov3 a, ov3 b, ov3 c, float* u, float
 }
 
 typedef struct { int32_t node; float dist; } leafpair; /* LeafNodePair (kd_tree.h:49-53) */
+static __thread int32_t* g_leaf_log = NULL; /* diagnostic leaf trace (om_primary_leaf_trace) */
+static __thread int32_t g_leaf_cap = 0, g_leaf_n = 0;
 
 typedef struct {
     int32_t* hit;     /* hit stack (node indices) */
@@ -488,6 +490,7 @@ static float tree_intersect(const om_tree* t, const oray* r, trav_ws* w, uint32_
     }
     for (int32_t j = 0; j < nleaf; j++) { /* :437-462 first improving leaf ends the scan */
         if (ctr) ctr->n_leaf++;
+        if (g_leaf_log && g_leaf_n < g_leaf_cap) g_leaf_log[g_leaf_n++] = lf[j].node;
         if (scan_leaf(t, &N[lf[j].node], r, &closest, face, u, v, ctr)) break;
     }
     return closest;
@@ -657,6 +660,28 @@ void om_primary_hits(const om_scene* s, const om_camera* cm, int32_t y0, int32_t
             t_out[k] = id.t;
         }
     }
+    ws_free(&w);
+}
+
+void om_primary_leaf_trace(const om_scene* s, const om_camera* cm, int32_t y0, int32_t y1,
+                           int32_t cap, int32_t* leaves_out, uint32_t* ntri_out) {
+    int32_t maxn = 1;
+    for (int32_t i = 0; i < s->nmodels; i++) if (s->models[i].tree && s->models[i].tree->nnodes > maxn) maxn = s->models[i].tree->nnodes;
+    trav_ws w; ws_init(&w, maxn);
+    for (int32_t y = y0; y < y1; y++) {
+        float fy = film_y(cm, y);
+        for (int32_t x = 0; x < cm->width; x++) {
+            size_t k = (size_t)(y - y0) * (size_t)cm->width + (size_t)x;
+            om_counters c; memset(&c, 0, sizeof(c));
+            g_leaf_log = leaves_out + k * (size_t)cap; g_leaf_cap = cap; g_leaf_n = 0;
+            for (int32_t q = 0; q < cap; q++) g_leaf_log[q] = -1;
+            ov3 d = primary_dir(cm, film_x(cm, x), fy);
+            isect id; memset(&id, 0, sizeof(id));
+            intersect_scene(s, cm->eye, d, &id, &w, &c);
+            ntri_out[k] = (uint32_t)c.n_tri;
+        }
+    }
+    g_leaf_log = NULL;
     ws_free(&w);
 }
 

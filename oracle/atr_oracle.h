@@ -105,6 +105,10 @@ void om_set_camera(om_camera* cm, ov3 eye, ov3 facing, int32_t w, int32_t h, int
 /* Primary-ray census over pixel rows [y0,y1): face (0xFFFFFFFF miss) and t bits per pixel. */
 void om_primary_hits(const om_scene* s, const om_camera* cm, int32_t y0, int32_t y1,
                      uint32_t* face_out, float* t_out, om_counters* ctr);
+/* Per-pixel trace of the primary ray's work: leaves scanned (in order, up to cap per pixel,
+   -1 padded) and triangle tests. Diagnostic for schedule modelling. */
+void om_primary_leaf_trace(const om_scene* s, const om_camera* cm, int32_t y0, int32_t y1,
+                           int32_t cap, int32_t* leaves_out, uint32_t* ntri_out);
 /* Arbitrary rays (origin+dir per ray, dir already normalized). */
 void om_trace_rays(const om_scene* s, const float* orig, const float* dir, int64_t n,
                    uint32_t* face_out, float* t_out, float* uv_out, om_counters* ctr);

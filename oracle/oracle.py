@@ -115,6 +115,8 @@ def lib():
                                     C.c_uint32, C.c_int32, C.c_float]
         L.om_primary_hits.argtypes = [P(om_scene), P(om_camera), C.c_int32, C.c_int32,
                                       C.c_void_p, C.c_void_p, P(om_counters)]
+        L.om_primary_leaf_trace.argtypes = [P(om_scene), P(om_camera), C.c_int32, C.c_int32,
+                                            C.c_int32, C.c_void_p, C.c_void_p]
         L.om_trace_rays.argtypes = [P(om_scene), C.c_void_p, C.c_void_p, C.c_int64,
                                     C.c_void_p, C.c_void_p, C.c_void_p, P(om_counters)]
         L.om_render_rows.argtypes = [P(om_scene), P(om_camera), C.c_uint64, C.c_int32, C.c_int32,
@@ -233,6 +235,15 @@ class Scene:
         lib().om_primary_hits(C.byref(self.s), C.byref(cam.c), y0, y1, _ptr(face), _ptr(t),
                               C.byref(ctr))
         return face.reshape(y1 - y0, cam.width), t.reshape(y1 - y0, cam.width), ctr.as_dict()
+
+    def leaf_trace(self, cam: Camera, cap=64):
+        """Per pixel: the leaves its primary ray scans (in order) and its triangle tests."""
+        n = cam.width * cam.height
+        leaves = np.empty((n, cap), np.int32)
+        ntri = np.empty(n, np.uint32)
+        lib().om_primary_leaf_trace(C.byref(self.s), C.byref(cam.c), 0, cam.height, cap,
+                                    _ptr(leaves), _ptr(ntri))
+        return leaves.reshape(cam.height, cam.width, cap), ntri.reshape(cam.height, cam.width)
 
     def trace(self, orig, dirs):
         orig = np.ascontiguousarray(orig, np.float32)

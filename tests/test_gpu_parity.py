@@ -229,3 +229,17 @@ def test_variants_agree_at_full_size_multibounce(eng):
         assert np.array_equal(a[k], b[k]) and np.array_equal(b[k], c[k])
     assert np.array_equal(a["rgb"].view(np.uint32), b["rgb"].view(np.uint32))
     assert a["traced"] == b["traced"] == c["traced"]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("name", ["monkey_1280x720_tree", "dragon_1920x1080_tree", "cube_256_tree",
+                                  "monkey_1280x720_bf"])
+def test_gpu_work_counters_equal_reference_work(eng, name, variant):
+    """The instrumented kernel's reference-equivalent work (box tests, triangle tests, leaves)
+    equals the oracle's counts of the reference algorithm on the same input -- the N_* of the
+    roofline byte model."""
+    g = GOLD["hits"][name]
+    upload(eng, g["asset"], g["tree"])
+    c = eng.counters(E.camera(g["W"], g["H"]), [[0, 0, g["W"] - 1, g["H"] - 1]], SEED, variant)
+    for k in ["n_rays", "n_box", "n_tri", "n_leaf"]:
+        assert c[k] == g["counters"][k], (k, c[k], g["counters"][k])
