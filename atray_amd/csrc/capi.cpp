@@ -175,6 +175,17 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     return &b;
 }
 
+// variant (atray.h) -> kernel schedule (render.hip). AUTO = the measured fastest.
+int sched_of(int32_t variant) {
+    switch (variant) {
+        case ATR_KERNEL_LANE: return 0;
+        case ATR_KERNEL_WAVE: return 1;
+        case ATR_KERNEL_TILE: return 2;
+        case ATR_KERNEL_TILE8: return 3;
+        default: return variant >= 16 ? variant : 0;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -577,8 +588,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     P.counters = nullptr;
-    // AUTO -> LANE (measured fastest); 16 + n = LANE at n waves/SIMD (diagnostic)
-    const int wave = variant >= 16 ? variant : (variant == ATR_KERNEL_WAVE ? 1 : 0);
+    const int wave = sched_of(variant);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(atr_launch_render(P, wave, s));
     HIPCHK(hipEventRecord(c->ev_stop, s));
@@ -613,7 +623,7 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.framebuffer = static_cast<uint32_t*>(fb);
     P.error_flag = c->d_error;
     P.counters = static_cast<unsigned long long*>(ctr);
-    HIPCHK(atr_launch_render(P, variant == ATR_KERNEL_WAVE ? 1 : 0, nullptr));
+    HIPCHK(atr_launch_render(P, sched_of(variant) >= 16 ? 0 : sched_of(variant), nullptr));
     HIPCHK(hipDeviceSynchronize());
     unsigned long long h[8];
     HIPCHK(hipMemcpy(h, ctr, sizeof(h), hipMemcpyDeviceToHost));

@@ -203,7 +203,7 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
         if (want == 0) break;
         const int src = __builtin_ctzll(want);
         const int32_t L = __builtin_amdgcn_readlane(leaf, src);  // uniform
-        if constexpr (COUNT) ct.wave_tri += m.leaf_range[2 * L + 1];  // every lane: wave-level count
+        if constexpr (COUNT) { if ((threadIdx.x & 63) == 0) ct.wave_tri += m.leaf_range[2 * L + 1]; }
         if (leaf == L) {
             const uint32_t first = m.leaf_range[2 * L], count = m.leaf_range[2 * L + 1];
             const bool hit = scan_leaf_uniform<COUNT>(r, m.tris, __builtin_amdgcn_readfirstlane(first),
@@ -214,8 +214,157 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
     }
 }
 
+// ------------------------------------------------------------------ TILE schedule
+// The NW waves of a workgroup (NW 8x8 cells) cooperate on leaf scans. Each round elects ONE
+// leaf that some ray of the workgroup wants next (at any position of its own sorted list),
+// compacts the rays that want it (ballot + per-wave prefix in LDS), stages the leaf's
+// triangles once in LDS (coalesced loads), and the waves process the compacted rays 64 per
+// wave, each lane testing every triangle of the leaf read by LDS broadcast. Every ray still
+// consumes its own leaves in its own sorted order and stops after the first leaf that
+// improves its hit (kd_tree.cpp:437-462), so results are identical to LANE; what changes is
+// that a leaf is fetched once per workgroup round instead of once per lane, and the triangle
+// loop reads LDS (no global-memory latency inside it).
+constexpr int kTileTris = 384;  // triangles staged per LDS chunk (Dragon's max leaf is 297)
+
+template <int NW>
+struct TileSmem {
+    float4_t t0[kTileTris], t1[kTileTris];
+    float t2[kTileTris];
+    float ray[6][NW * 64];            // o.xyz, d.xyz per thread
+    float rt[NW * 64], ru[NW * 64], rv[NW * 64];
+    uint32_t rslot[NW * 64];
+    int32_t list[NW * 64];
+    int32_t cand[NW], cnt[NW];
+};
+
+template <int NW, bool COUNT>
+__device__ __forceinline__ int32_t tile_next_leaf(TreeQuery& q, const Ray& r, const DModel& m, int& err,
+                                                  Ctr& ct) {
+    // pop the scanned head; refill with a re-walk after the bound when the buffer runs dry
+    for (;;) {
+        if (q.state == 2) return -1;
+        if (q.state == 0) {
+            q.ncand = traverse_pass<kLeafBuf, COUNT>(r, m.nodes, q.lb, q.bd, q.bi, ct);
+            if (q.ncand < 0) { err = 1; q.state = 2; return -1; }
+            q.pos = q.ncand < kLeafBuf ? q.ncand : kLeafBuf;  // entries left in the buffer
+            q.state = 1;
+            if (q.pos > 0) return q.lb.node[0];
+        }
+        if (q.pos > 0) return q.lb.node[0];
+        if (q.ncand <= kLeafBuf) { q.state = 2; return -1; }
+        q.state = 0;
+    }
+}
+
+template <int NW, bool COUNT>
+__device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m, bool active, Hit& h,
+                                                  int& err, Ctr& ct) {
+    constexpr int NT = NW * 64;
+    __shared__ TileSmem<NW> sm;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    h.t = kMaxFloat;
+    h.face = 0;
+    h.u = h.v = 0.f;
+    TreeQuery q;
+    q.state = 2;
+    q.pos = 0;
+    q.ncand = 0;
+    bool root_scan = false;
+    int32_t my_leaf = -1;
+    uint32_t slot = 0xFFFFFFFFu;
+    if (active) {
+        const NodeBox root = load_node(m.nodes, 0);
+        if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
+        if (box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) {  // :339
+            if (root.children == 0) { root_scan = true; my_leaf = 0; }
+            else {
+                q.bd = -__builtin_inff();
+                q.bi = -1;
+                q.state = 0;
+                my_leaf = tile_next_leaf<NW, COUNT>(q, r, m, err, ct);
+            }
+        }
+    }
+    sm.ray[0][tid] = r.o.x; sm.ray[1][tid] = r.o.y; sm.ray[2][tid] = r.o.z;
+    sm.ray[3][tid] = r.d.x; sm.ray[4][tid] = r.d.y; sm.ray[5][tid] = r.d.z;
+    for (;;) {
+        const uint64_t want = __ballot(my_leaf >= 0);
+        if (lane == 0) sm.cand[w] = want ? __builtin_amdgcn_readlane(my_leaf, __builtin_ctzll(want)) : 0x7FFFFFFF;
+        __syncthreads();
+        int32_t L = 0x7FFFFFFF;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) L = sm.cand[i] < L ? sm.cand[i] : L;
+        if (L == 0x7FFFFFFF) break;  // workgroup-uniform
+        const bool mem = my_leaf == L;
+        const uint64_t mb = __ballot(mem);
+        if (lane == 0) sm.cnt[w] = __popcll(mb);
+        const uint32_t first = m.leaf_range[2 * L], count = m.leaf_range[2 * L + 1];
+        __syncthreads();
+        int32_t base = 0, n = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) { base += i < w ? sm.cnt[i] : 0; n += sm.cnt[i]; }
+        if (mem) sm.list[base + __popcll(mb & ((uint64_t(1) << lane) - 1))] = tid;
+        if constexpr (COUNT) {
+            if (tid == 0) ct.wave_tri += uint32_t((n + 63) / 64) * count;
+        }
+        for (uint32_t c0 = 0; c0 < count; c0 += kTileTris) {
+            const uint32_t cc = count - c0 < uint32_t(kTileTris) ? count - c0 : uint32_t(kTileTris);
+            for (uint32_t i = tid; i < cc; i += NT) {
+                sm.t0[i] = m.t0[first + c0 + i];
+                sm.t1[i] = m.t1[first + c0 + i];
+                sm.t2[i] = m.t2[first + c0 + i];
+            }
+            __syncthreads();
+            for (int ch = w; ch * 64 < n; ch += NW) {
+                const int idx = ch * 64 + lane;
+                if (idx < n) {
+                    const int mt = sm.list[idx];
+                    Ray rr;
+                    rr.o = mk(sm.ray[0][mt], sm.ray[1][mt], sm.ray[2][mt]);
+                    rr.d = mk(sm.ray[3][mt], sm.ray[4][mt], sm.ray[5][mt]);
+                    float bt = kMaxFloat, bu = 0.f, bv = 0.f;
+                    uint32_t bs = 0xFFFFFFFFu;
+                    if (c0 > 0) { bt = sm.rt[mt]; bu = sm.ru[mt]; bv = sm.rv[mt]; bs = sm.rslot[mt]; }
+                    for (uint32_t k = 0; k < cc; ++k) {
+                        const float4_t a = sm.t0[k], b = sm.t1[k];
+                        const float c = sm.t2[k];
+                        float u = 0.f, v = 0.f;
+                        const float dist = tri_hit(rr, mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), mk(b.z, b.w, c), u, v);
+                        if (dist < bt && dist > kTol) { bt = dist; bs = first + c0 + k; bu = u; bv = v; }
+                    }
+                    sm.rt[mt] = bt; sm.ru[mt] = bu; sm.rv[mt] = bv; sm.rslot[mt] = bs;
+                }
+            }
+            __syncthreads();
+        }
+        if (mem) {
+            if constexpr (COUNT) { ct.tri += count; ct.leaf += 1; }
+            const bool improved = count > 0 && sm.rt[tid] < kMaxFloat;
+            if (improved) {
+                h.t = sm.rt[tid]; h.u = sm.ru[tid]; h.v = sm.rv[tid];
+                slot = sm.rslot[tid];
+                my_leaf = -1;
+                q.state = 2;
+            } else if (root_scan) {
+                my_leaf = -1;
+            } else {
+                q.bd = q.lb.d[0];
+                q.bi = q.lb.idx[0];
+                lb_pop<kLeafBuf>(q.lb);
+                --q.pos;
+                my_leaf = tile_next_leaf<NW, COUNT>(q, r, m, err, ct);
+            }
+        }
+    }
+    if (slot != 0xFFFFFFFFu) h.face = m.tface[slot];
+}
+
 // ------------------------------------------------------------------ get_intersection_data
-template <bool WAVE, bool COUNT>
+enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3 };
+constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
+constexpr bool sched_coop(int sc) { return sc != SCHED_LANE; }  // lanes must stay in lockstep loops
+
+template <int SCHED, bool COUNT>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
                                                 Isect& id, int& err, Ctr& ct) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
@@ -228,7 +377,9 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
         const DModel& m = S->models[i];
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
             Hit h;
-            if (WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
+            if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
+            else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
+            else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if (active) tree_closest_lane<COUNT>(r, m, h, err, ct);
             else h.t = kMaxFloat;
             if (h.t > kTol && h.t < best) { best = h.t; face = h.face; fu = h.u; fv = h.v; nm = i; }
@@ -306,7 +457,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
 }
 
 // ------------------------------------------------------------------ cast_ray + pixel loop
-template <bool WAVE, bool COUNT>
+template <int SCHED, bool COUNT>
 __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d, int32_t bounce_limit,
                                        bool active, uint64_t& st, uint64_t stream, uint32_t& casts,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
@@ -318,11 +469,12 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
     // cooperate on leaf scans inside intersect_scene.
     for (i = 0; ; ++i) {
         const bool go = live && i < bounce_limit;
-        if (WAVE) { if (__ballot(go) == 0) break; }
+        if constexpr (SCHED == SCHED_WAVE) { if (__ballot(go) == 0) break; }
+        else if constexpr (sched_coop(SCHED)) { if (!__syncthreads_or(go)) break; }
         else if (!go) break;
         Isect id;
         id.type = T_NONE;
-        intersect_scene<WAVE, COUNT>(S, o, d, go, id, err, ct);
+        intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct);
         if (!go) continue;
         ++traced;
         if (record && i == 0) { hit_face = id.face; hit_t = id.t; }
@@ -364,12 +516,16 @@ __device__ __forceinline__ int remap_xcd(int wg, int nwg) {
 // feed only a second iteration that never runs (renderer.cpp:222-259), so they are skipped --
 // output bit-identical, and far fewer live registers. Every sample re-traces the same primary
 // ray in the reference (:353-356) and sums the same color, reproduced by the same f32 adds.
-template <bool WAVE, bool COUNT, bool PRIMARY, int OCC = 4>
-__global__ __launch_bounds__(256, OCC) void render_kernel(RenderParams P) {
+template <int SCHED, bool COUNT, bool PRIMARY, int OCC = 4>
+__global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(RenderParams P) {
+    constexpr int NW = sched_waves(SCHED);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = remap_xcd(blockIdx.x, gridDim.x) * 4 + wave;
-    if (b >= P.nblocks) return;  // whole wavefront
-    const DBlock blk = P.blocks[b];
+    const int b = remap_xcd(blockIdx.x, gridDim.x) * NW + wave;
+    if (SCHED != SCHED_TILE4 && SCHED != SCHED_TILE8 && b >= P.nblocks) return;  // whole wavefront
+    const bool in_range = b < P.nblocks;
+    DBlock blk;
+    if (in_range) blk = P.blocks[b];
+    else { blk.x0 = 0; blk.y0 = 0; blk.mask_lo = 0; blk.mask_hi = 0; blk.out_base = 0; }
     const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
     const bool active = (mask >> lane) & 1;
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
@@ -390,7 +546,7 @@ __global__ __launch_bounds__(256, OCC) void render_kernel(RenderParams P) {
     if constexpr (PRIMARY) {
         Isect id;
         id.type = T_NONE;
-        intersect_scene<WAVE, COUNT>(S, eye, dir, active, id, err, ct);
+        intersect_scene<SCHED, COUNT>(S, eye, dir, active, id, err, ct);
         if (active) {
             const DMaterial& mat = S->mats[id.material];
             const V3 ret = mk(mat.ex, mat.ey, mat.ez);  // weight (1,1,1) x emission
@@ -410,7 +566,7 @@ __global__ __launch_bounds__(256, OCC) void render_kernel(RenderParams P) {
             const float yo = rand_bi(st, stream) * cm.half_pixel_height + film_y;
             dir = unit(sub(add(add(fc, scale(cx, xo)), scale(cy, yo)), eye));
         }
-        col = add(col, cast_ray<WAVE, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
+        col = add(col, cast_ray<SCHED, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
                                              s == 0, hit_face, hit_t, err, ct));
     }
     if (active) {
@@ -443,7 +599,6 @@ __global__ __launch_bounds__(256, OCC) void render_kernel(RenderParams P) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             uint32_t t = v[k];
-            if (k == 3) t = (lane == 0) ? t : 0u;  // wave-level count: every lane holds the same value
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
             if (lane == 0 && t) atomicAdd(C + 1 + k, (unsigned long long)t);
@@ -451,17 +606,18 @@ __global__ __launch_bounds__(256, OCC) void render_kernel(RenderParams P) {
         uint32_t t = traced;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-        if (lane == 0) { atomicAdd(C + 0, (unsigned long long)t); atomicAdd(C + 7, 1ull); }
+        if (lane == 0) { atomicAdd(C + 0, (unsigned long long)t); if (in_range) atomicAdd(C + 7, 1ull); }
     }
 }
 
-#define ATR_INST(W, C, PR) template __global__ void render_kernel<W, C, PR>(RenderParams);
-ATR_INST(false, false, false) ATR_INST(true, false, false) ATR_INST(false, true, false) ATR_INST(true, true, false)
-ATR_INST(false, false, true) ATR_INST(true, false, true) ATR_INST(false, true, true) ATR_INST(true, true, true)
+#define ATR_INST(SC, C, PR) template __global__ void render_kernel<SC, C, PR>(RenderParams);
+#define ATR_INST4(SC) ATR_INST(SC, false, false) ATR_INST(SC, true, false) ATR_INST(SC, false, true) ATR_INST(SC, true, true)
+ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCHED_TILE8)
+#undef ATR_INST4
 #undef ATR_INST
-template __global__ void render_kernel<false, false, true, 5>(RenderParams);
-template __global__ void render_kernel<false, false, true, 6>(RenderParams);
-template __global__ void render_kernel<false, false, true, 8>(RenderParams);
+template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_LANE, false, true, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_LANE, false, true, 8>(RenderParams);
 
 __global__ __launch_bounds__(256) void unpack_kernel(const DBlock* __restrict__ blocks, int32_t nblocks,
                                                      int32_t width, const uint32_t* __restrict__ packed,
@@ -501,30 +657,38 @@ __global__ __launch_bounds__(256) void tile_casts_kernel(const atr_tile* __restr
 // Default occupancy of the PRIMARY lane kernel (waves/SIMD; chosen by measurement).
 constexpr int kPrimaryOcc = 5;
 
-extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s) {
-    const int grid = (P.nblocks + 3) / 4;
-    if (grid <= 0) return hipSuccess;
-    const int occ = wave >= 16 ? wave - 16 : (wave ? 0 : kPrimaryOcc);  // 16+occ: explicit occupancy
-    if (wave >= 16) wave = 0;
+template <int SC, bool C, bool PR>
+static void launch_one(const atr::RenderParams& P, hipStream_t s) {
+    constexpr int NW = atr::sched_waves(SC);
+    const int grid = (P.nblocks + NW - 1) / NW;
+    hipLaunchKernelGGL((atr::render_kernel<SC, C, PR>), dim3(grid), dim3(64 * NW), 0, s, P);
+}
+
+template <int SC>
+static void launch_sched(const atr::RenderParams& P, bool count, bool prim, hipStream_t s) {
+    if (count) { if (prim) launch_one<SC, true, true>(P, s); else launch_one<SC, true, false>(P, s); }
+    else { if (prim) launch_one<SC, false, true>(P, s); else launch_one<SC, false, false>(P, s); }
+}
+
+// sched: 0 LANE, 1 WAVE, 2 TILE4, 3 TILE8; 16 + n: LANE at n waves/SIMD (diagnostic)
+extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, hipStream_t s) {
+    if (P.nblocks <= 0) return hipSuccess;
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
-    const int key = (wave ? 4 : 0) | (count ? 2 : 0) | (prim ? 1 : 0);
-    const dim3 g(grid), b(256);
-    if (key == 1 && occ != 4) {
-        if (occ == 5) hipLaunchKernelGGL((atr::render_kernel<false, false, true, 5>), g, b, 0, s, P);
-        else if (occ == 6) hipLaunchKernelGGL((atr::render_kernel<false, false, true, 6>), g, b, 0, s, P);
-        else hipLaunchKernelGGL((atr::render_kernel<false, false, true, 8>), g, b, 0, s, P);
+    const dim3 g((P.nblocks + 3) / 4), b(256);
+    int occ = sched >= 16 ? sched - 16 : (sched == 0 ? kPrimaryOcc : 0);
+    if (sched >= 16) sched = 0;
+    if (sched == 0 && prim && !count && occ != 4) {
+        if (occ == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_LANE, false, true, 5>), g, b, 0, s, P);
+        else if (occ == 6) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_LANE, false, true, 6>), g, b, 0, s, P);
+        else hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_LANE, false, true, 8>), g, b, 0, s, P);
         return hipGetLastError();
     }
-    switch (key) {
-        case 0: hipLaunchKernelGGL((atr::render_kernel<false, false, false>), g, b, 0, s, P); break;
-        case 1: hipLaunchKernelGGL((atr::render_kernel<false, false, true>), g, b, 0, s, P); break;
-        case 2: hipLaunchKernelGGL((atr::render_kernel<false, true, false>), g, b, 0, s, P); break;
-        case 3: hipLaunchKernelGGL((atr::render_kernel<false, true, true>), g, b, 0, s, P); break;
-        case 4: hipLaunchKernelGGL((atr::render_kernel<true, false, false>), g, b, 0, s, P); break;
-        case 5: hipLaunchKernelGGL((atr::render_kernel<true, false, true>), g, b, 0, s, P); break;
-        case 6: hipLaunchKernelGGL((atr::render_kernel<true, true, false>), g, b, 0, s, P); break;
-        default: hipLaunchKernelGGL((atr::render_kernel<true, true, true>), g, b, 0, s, P); break;
+    switch (sched) {
+        case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
+        case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;
+        case 3: launch_sched<atr::SCHED_TILE8>(P, count, prim, s); break;
+        default: launch_sched<atr::SCHED_LANE>(P, count, prim, s); break;
     }
     return hipGetLastError();
 }

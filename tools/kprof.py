@@ -43,7 +43,8 @@ def main():
     fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, None, None)
     stream = torch.cuda.current_stream().cuda_stream
-    names = {"lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE, "occ4": 20, "occ5": 21,
+    names = {"lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE, "tile": E.ATR_KERNEL_TILE,
+             "tile8": E.ATR_KERNEL_TILE8, "occ4": 20, "occ5": 21,
              "occ6": 22, "occ8": 24}
     vs = args.variants.split(",")
     res = {v: [] for v in vs}
