@@ -13,12 +13,15 @@
 
 #include "engine.h"
 #include "host_scene.h"
+#include "wavefront.h"
 
 using namespace atr;
 
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s);
 extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                         const uint32_t* packed, uint32_t* image, hipStream_t s);
+extern "C" hipError_t atr_wf_render(const atr::WFParams& W, int32_t nmodels, const int32_t* nnodes,
+                                    const int32_t* has_tree, int32_t* pinned, hipStream_t s);
 extern "C" hipError_t atr_launch_tile_casts(const atr_tile* tiles, int32_t ntiles, int32_t width,
                                             const uint32_t* casts, int64_t* out, hipStream_t s);
 
@@ -43,6 +46,7 @@ struct BlockSet {
     std::vector<DBlock> host;
     DevBuf dev;
     DevBuf dev_tiles;
+    DevBuf dev_pix;  // pixel index per packed slot (wavefront schedule)
     int64_t packed_pixels = 0;
 };
 
@@ -112,6 +116,12 @@ struct atr_ctx {
     uint64_t block_use[kBlockSlots] = {};
     uint64_t use_clock = 0;
     int32_t* d_error = nullptr;
+    // wavefront workspace (grown on demand)
+    DevBuf wf_mem;
+    int64_t wf_n = 0, wf_nodes = 0;
+    atr::WFParams wf = {};
+    int32_t* wf_pinned = nullptr;
+    std::vector<int32_t> model_nodes, model_tree;
 };
 
 namespace {
@@ -124,6 +134,70 @@ int dev_upload(atr_ctx* c, const void* src, size_t bytes, void** out) {
     c->scene_bufs.push_back(b);
     c->scene_bytes += int64_t(b.n);
     *out = b.p;
+    return ATR_OK;
+}
+
+// Carve the wavefront workspace for n path slots and a tree of `nodes` nodes.
+int wf_reserve(atr_ctx* c, int64_t n, int64_t nodes) {
+    if (n <= c->wf_n && nodes <= c->wf_nodes && c->wf_mem.p) return ATR_OK;
+    if (c->have_render) HIPCHK(hipEventSynchronize(c->ev_done));
+    if (c->wf_mem.p) HIPCHK(hipFree(c->wf_mem.p));
+    c->wf_mem = DevBuf();
+    n = std::max<int64_t>(n, c->wf_n);
+    nodes = std::max<int64_t>(nodes, c->wf_nodes);
+    const int64_t items = n / 64 + nodes + 64;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_rng = take(8 * n), o_col = take(12 * n), o_ret = take(12 * n), o_wt = take(12 * n),
+                 o_casts = take(4 * n), o_traced = take(4 * n), o_hface = take(4 * n), o_ht = take(4 * n),
+                 o_ro = take(12 * n), o_rd = take(12 * n), o_bt = take(4 * n), o_bu = take(4 * n),
+                 o_bv = take(4 * n), o_bface = take(4 * n), o_bmodel = take(4 * n), o_ql = take(32 * n),
+                 o_qd7 = take(4 * n), o_qi7 = take(4 * n), o_qpos = take(4 * n), o_qnb = take(4 * n),
+                 o_qnc = take(4 * n), o_pleaf = take(4 * n), o_pslot = take(4 * n), o_act0 = take(4 * n),
+                 o_act1 = take(4 * n), o_pend0 = take(4 * n), o_pend1 = take(4 * n), o_rw = take(4 * n),
+                 o_cnt0 = take(4 * nodes), o_cnt1 = take(4 * nodes), o_offs = take(4 * nodes),
+                 o_items = take(16 * (nodes + 64)), o_bucket = take(4 * n), o_ctl = take(sizeof(WFCtl));
+    HIPCHK(hipMalloc(&c->wf_mem.p, off));
+    c->wf_mem.n = off;
+    HIPCHK(hipMemset(c->wf_mem.p, 0, off));
+    char* b = static_cast<char*>(c->wf_mem.p);
+    WFParams& W = c->wf;
+    W.rng = reinterpret_cast<uint64_t*>(b + o_rng);
+    W.col = reinterpret_cast<float*>(b + o_col);
+    W.ret = reinterpret_cast<float*>(b + o_ret);
+    W.wt = reinterpret_cast<float*>(b + o_wt);
+    W.casts = reinterpret_cast<uint32_t*>(b + o_casts);
+    W.traced = reinterpret_cast<uint32_t*>(b + o_traced);
+    W.hface = reinterpret_cast<uint32_t*>(b + o_hface);
+    W.ht = reinterpret_cast<float*>(b + o_ht);
+    W.ro = reinterpret_cast<float*>(b + o_ro);
+    W.rd = reinterpret_cast<float*>(b + o_rd);
+    W.bt = reinterpret_cast<float*>(b + o_bt);
+    W.bu = reinterpret_cast<float*>(b + o_bu);
+    W.bv = reinterpret_cast<float*>(b + o_bv);
+    W.bface = reinterpret_cast<uint32_t*>(b + o_bface);
+    W.bmodel = reinterpret_cast<int32_t*>(b + o_bmodel);
+    W.ql = reinterpret_cast<int32_t*>(b + o_ql);
+    W.qd7 = reinterpret_cast<float*>(b + o_qd7);
+    W.qi7 = reinterpret_cast<int32_t*>(b + o_qi7);
+    W.qpos = reinterpret_cast<int32_t*>(b + o_qpos);
+    W.qnb = reinterpret_cast<int32_t*>(b + o_qnb);
+    W.qnc = reinterpret_cast<int32_t*>(b + o_qnc);
+    W.pleaf = reinterpret_cast<int32_t*>(b + o_pleaf);
+    W.pslot = reinterpret_cast<int32_t*>(b + o_pslot);
+    W.act[0] = reinterpret_cast<int32_t*>(b + o_act0);
+    W.act[1] = reinterpret_cast<int32_t*>(b + o_act1);
+    W.pend[0] = reinterpret_cast<int32_t*>(b + o_pend0);
+    W.pend[1] = reinterpret_cast<int32_t*>(b + o_pend1);
+    W.rw = reinterpret_cast<int32_t*>(b + o_rw);
+    W.cnt[0] = reinterpret_cast<uint32_t*>(b + o_cnt0);
+    W.cnt[1] = reinterpret_cast<uint32_t*>(b + o_cnt1);
+    W.offs = reinterpret_cast<int32_t*>(b + o_offs);
+    W.items = reinterpret_cast<int32_t*>(b + o_items);
+    W.bucket = reinterpret_cast<int32_t*>(b + o_bucket);
+    W.ctl = reinterpret_cast<WFCtl*>(b + o_ctl);
+    c->wf_n = n;
+    c->wf_nodes = nodes;
     return ATR_OK;
 }
 
@@ -167,6 +241,25 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
         b.dev_tiles = DevBuf();
         if (hipMalloc(&b.dev_tiles.p, tneed) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
         b.dev_tiles.n = tneed;
+    }
+    {   // pixel of every packed slot, in slot order
+        std::vector<int32_t> pix(size_t(b.packed_pixels > 0 ? b.packed_pixels : 1), 0);
+        size_t k = 0;
+        for (const DBlock& blk : b.host) {
+            const uint64_t m = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+            for (int lane = 0; lane < 64; ++lane)
+                if ((m >> lane) & 1) pix[k++] = (blk.y0 + (lane >> 3)) * W + (blk.x0 + (lane & 7));
+        }
+        const size_t pneed = pix.size() * sizeof(int32_t);
+        if (b.dev_pix.n < pneed) {
+            if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
+            b.dev_pix = DevBuf();
+            if (hipMalloc(&b.dev_pix.p, pneed) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
+            b.dev_pix.n = pneed;
+        }
+        if (hipMemcpy(b.dev_pix.p, pix.data(), pneed, hipMemcpyHostToDevice) != hipSuccess) {
+            rc = ATR_E_NOMEM; b.width = -1; return nullptr;
+        }
     }
     hipError_t e = hipMemcpy(b.dev.p, b.host.data(), b.host.size() * sizeof(DBlock), hipMemcpyHostToDevice);
     if (e == hipSuccess && ntiles)
@@ -352,7 +445,10 @@ int atr_destroy(atr_ctx* c) {
     for (BlockSet& b : c->blocks) {
         if (b.dev.p) (void)hipFree(b.dev.p);
         if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
+        if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
     }
+    if (c->wf_mem.p) (void)hipFree(c->wf_mem.p);
+    if (c->wf_pinned) (void)hipHostFree(c->wf_pinned);
     if (c->d_error) (void)hipFree(c->d_error);
     (void)hipEventDestroy(c->ev_start);
     (void)hipEventDestroy(c->ev_stop);
@@ -517,6 +613,11 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
         c->d_scene = static_cast<DScene*>(p);
     }
     c->nmodels = nmodels;
+    c->model_nodes.assign(size_t(nmodels), 1);
+    c->model_tree.assign(size_t(nmodels), 0);
+    for (int32_t i = 0; i < nmodels; ++i) {
+        if (models[i].tree) { c->model_nodes[size_t(i)] = models[i].tree->t.nnodes; c->model_tree[size_t(i)] = 1; }
+    }
     return ATR_OK;
 }
 
@@ -572,6 +673,35 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     int rc = ATR_OK;
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
+    if (variant == ATR_KERNEL_WAVEFRONT) {
+        int64_t maxn = 1;
+        for (int32_t v : c->model_nodes) maxn = std::max<int64_t>(maxn, v);
+        if ((rc = wf_reserve(c, std::max<int64_t>(bs->packed_pixels, 1), maxn))) return rc;
+        if (!c->wf_pinned) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->wf_pinned), 64));
+        WFParams W = c->wf;
+        W.cam = *cam;
+        W.scene = c->d_scene;
+        W.seed = seed;
+        W.n = int32_t(bs->packed_pixels);
+        W.layout = fr->layout;
+        W.pix = static_cast<const int32_t*>(bs->dev_pix.p);
+        W.framebuffer = fr->framebuffer;
+        W.out_hit_face = fr->hit_face;
+        W.out_hit_t = fr->hit_t;
+        W.out_rgb = fr->rgb;
+        W.out_ray_casts = fr->ray_casts;
+        W.traced_rays = fr->traced_rays;
+        W.error_flag = c->d_error;
+        HIPCHK(hipEventRecord(c->ev_start, s));
+        if (W.n > 0)
+            HIPCHK(atr_wf_render(W, c->nmodels, c->model_nodes.data(), c->model_tree.data(), c->wf_pinned, s));
+        HIPCHK(hipEventRecord(c->ev_stop, s));
+        HIPCHK(hipEventRecord(c->ev_done, s));
+        c->have_render = true;
+        c->last_stream = s;
+        c->last_ntiles = ntiles;
+        return ATR_OK;
+    }
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;

@@ -25,7 +25,6 @@ struct Isect {
     uint32_t face;
 };
 
-constexpr int kLeafBuf = 8;
 
 // ------------------------------------------------------------------ LANE schedule
 // Per-lane leaf scan over the SoA triangle streams, one triangle of prefetch: the loads of

@@ -143,6 +143,8 @@ __device__ __forceinline__ bool scan_leaf(const Ray& r, const DTri* __restrict__
 }
 
 // ------------------------------------------------------------------ leaf order buffer
+constexpr int kLeafBuf = 8;  // sorted leaves held per ray between DFS passes
+
 template <int K>
 struct LeafBuf {
     float d[K];

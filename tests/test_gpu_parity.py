@@ -14,7 +14,8 @@ from tests.goldens import GOLD, SEED, hits, render  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 SKY, MODEL = O.SKY, O.MODEL_MAT
-VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8]
+VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8,
+            E.ATR_KERNEL_WAVEFRONT]
 RGB_RTOL = 1e-5
 
 
