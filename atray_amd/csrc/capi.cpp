@@ -4,6 +4,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -111,6 +112,8 @@ struct atr_ctx {
     DScene* d_scene = nullptr;
     int64_t scene_bytes = 0;
     int32_t max_nodes = 0, max_depth = 0, nmodels = 0;
+    int cluster_size = 16;     // primitives per leaf cluster (ATR_CLUSTER_SIZE overrides, 1..32)
+    int64_t nclusters = 0;
     static constexpr int kBlockSlots = 24;  // tile-list cache: own render + one unpack per rank
     BlockSet blocks[kBlockSlots];
     uint64_t block_use[kBlockSlots] = {};
@@ -145,7 +148,6 @@ int wf_reserve(atr_ctx* c, int64_t n, int64_t nodes) {
     c->wf_mem = DevBuf();
     n = std::max<int64_t>(n, c->wf_n);
     nodes = std::max<int64_t>(nodes, c->wf_nodes);
-    const int64_t items = n / 64 + nodes + 64;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_rng = take(8 * n), o_col = take(12 * n), o_ret = take(12 * n), o_wt = take(12 * n),
@@ -275,6 +277,8 @@ int sched_of(int32_t variant) {
         case ATR_KERNEL_WAVE: return 1;
         case ATR_KERNEL_TILE: return 2;
         case ATR_KERNEL_TILE8: return 3;
+        case ATR_KERNEL_CLUSTER: return 4;
+        case ATR_KERNEL_AUTO: return 4;  // CLUSTER: fastest measured
         default: return variant >= 16 ? variant : 0;
     }
 }
@@ -486,6 +490,11 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
     S.nmodels = nmodels;
     c->max_nodes = 0;
     c->max_depth = 0;
+    c->nclusters = 0;
+    if (const char* e = std::getenv("ATR_CLUSTER_SIZE")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= 32) c->cluster_size = v;
+    }
     for (int32_t i = 0; i < nmodels; ++i) {
         const atr_model& md = models[i];
         const HostMesh& M = md.mesh->m;
@@ -565,6 +574,38 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 dm.t2 = static_cast<const float*>(p);
                 if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
                 dm.tface = static_cast<const uint32_t*>(p);
+            }
+            {  // clustered copy of the leaf primitives
+                LeafClusters C;
+                if ((rc = leaf_clusters(T, c->cluster_size, C))) return rc;
+                const size_t ns = C.order.size() ? C.order.size() : 1;
+                std::vector<float4_t> s0(ns), s1(ns);
+                std::vector<float4_t> s2(ns);
+                std::vector<uint32_t> sf(ns, 0u), sr(ns, 0u);
+                for (size_t k = 0; k < C.order.size(); ++k) {
+                    const DTri& t = tris[C.order[k]];
+                    s0[k] = float4_t{t.ax, t.ay, t.az, t.abx};
+                    s1[k] = float4_t{t.aby, t.abz, t.acx, t.acy};
+                    s2[k] = float4_t{C.normal[3 * k], C.normal[3 * k + 1], C.normal[3 * k + 2], t.acz};
+                    sf[k] = t.face;
+                    sr[k] = C.rank[k];
+                }
+                if (C.rec.empty()) C.rec.assign(8, 0.f);
+                if ((rc = dev_upload(c, C.rec.data(), C.rec.size() * sizeof(float), &p))) return rc;
+                dm.clus = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, C.range.data(), C.range.size() * sizeof(uint32_t), &p))) return rc;
+                dm.cl_range = static_cast<const uint32_t*>(p);
+                if ((rc = dev_upload(c, s0.data(), s0.size() * sizeof(float4_t), &p))) return rc;
+                dm.c0 = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
+                dm.c1 = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, s2.data(), s2.size() * sizeof(float4_t), &p))) return rc;
+                dm.c2 = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
+                dm.cface = static_cast<const uint32_t*>(p);
+                if ((rc = dev_upload(c, sr.data(), sr.size() * sizeof(uint32_t), &p))) return rc;
+                dm.crank = static_cast<const uint32_t*>(p);
+                c->nclusters += int64_t(C.rec.size() / 8);
             }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
             dm.nodes = static_cast<const DNode*>(p);

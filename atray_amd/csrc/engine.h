@@ -98,6 +98,17 @@ struct DModel {
     const float4_t* t1;
     const float* t2;
     const uint32_t* tface;
+    // leaf clusters, 2 float4 per cluster: {lo.xyz, bound of |ab||ac| with
+    // (n - 1) in its low 5 mantissa bits}, {hi.xyz, bits(first slot)}; cl_range = first
+    // cluster, count per node; the primitives again in cluster order: c0 = {a.xyz, ab.x},
+    // c1 = {ab.yz, ac.xy}, c2 = {n = ab x ac, ac.z}, their faces and leaf ranks
+    const float4_t* clus;
+    const uint32_t* cl_range;
+    const float4_t* c0;
+    const float4_t* c1;
+    const float4_t* c2;
+    const uint32_t* cface;
+    const uint32_t* crank;
     const float* shade;          // 9 f32 per face: smooth -> na, nb, nc; flat -> v0, v1, v2
     uint32_t nfaces;
     int32_t has_tree;

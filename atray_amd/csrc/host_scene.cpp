@@ -2,11 +2,13 @@
 // OBJ loading with the reference's number parser, model AABB/translation, the octree build
 // and its flattening into the device layout of engine.h. Reference: OBJ_loader.cpp:278-360,
 // utilities/parser.h, model.h:41-61,136-152, kd_tree.cpp:1-288, camera.h, renderer.cpp:403-445.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "engine.h"
@@ -260,6 +262,101 @@ int atr::octree_build(const HostMesh& m, uint32_t max_faces, HostTree& T) {
                 T.prim_face.push_back(t.face);
             }
         }
+    }
+    return ATR_OK;
+}
+
+int atr::leaf_clusters(const HostTree& T, int size, LeafClusters& C) {
+    if (size < 1 || size > 32) return ATR_E_INVALID;
+    const size_t np = T.prim_face.size();
+    C = LeafClusters();
+    C.order.reserve(np);
+    C.rank.reserve(np);
+    C.range.assign(2 * size_t(T.nnodes), 0u);
+    const float* V = T.prim_vertices.data();
+    for (size_t k = 0; k < 9 * np; ++k) C.max_abs = std::max(C.max_abs, std::fabs(V[k]));
+    std::vector<uint32_t> idx;
+    std::vector<double> cen;
+    for (int32_t n = 0; n < T.nnodes; ++n) {
+        if (T.children[size_t(n)]) continue;
+        const uint32_t first = T.leaf_first[size_t(n)], cnt = T.leaf_count[size_t(n)];
+        C.range[2 * size_t(n)] = uint32_t(C.rec.size() / 8);
+        if (!cnt) continue;
+        idx.resize(cnt);
+        cen.resize(3 * size_t(cnt));
+        for (uint32_t i = 0; i < cnt; ++i) {
+            idx[i] = i;
+            const float* v = V + 9 * size_t(first + i);
+            for (int a = 0; a < 3; ++a) cen[3 * i + a] = (double(v[a]) + v[3 + a] + v[6 + a]) / 3.0;
+        }
+        // explicit stack of [lo, hi) ranges; children pushed right-first so clusters come out
+        // left to right
+        std::vector<std::pair<uint32_t, uint32_t>> st{{0u, cnt}};
+        while (!st.empty()) {
+            const auto [lo, hi] = st.back();
+            st.pop_back();
+            const uint32_t m = hi - lo;
+            if (m > uint32_t(size)) {
+                double bl[3] = {1e300, 1e300, 1e300}, bh[3] = {-1e300, -1e300, -1e300};
+                for (uint32_t i = lo; i < hi; ++i)
+                    for (int a = 0; a < 3; ++a) {
+                        bl[a] = std::min(bl[a], cen[3 * idx[i] + a]);
+                        bh[a] = std::max(bh[a], cen[3 * idx[i] + a]);
+                    }
+                int ax = 0;
+                for (int a = 1; a < 3; ++a)
+                    if (bh[a] - bl[a] > bh[ax] - bl[ax]) ax = a;
+                const uint32_t nclus = (m + uint32_t(size) - 1) / uint32_t(size);
+                const uint32_t left = ((nclus + 1) / 2) * uint32_t(size);
+                std::nth_element(idx.begin() + lo, idx.begin() + lo + left, idx.begin() + hi,
+                                 [&](uint32_t x, uint32_t y) {
+                                     const double cx = cen[3 * x + ax], cy = cen[3 * y + ax];
+                                     return cx < cy || (cx == cy && x < y);
+                                 });
+                st.push_back({lo + left, hi});
+                st.push_back({lo, lo + left});
+                continue;
+            }
+            std::sort(idx.begin() + lo, idx.begin() + hi);  // leaf order inside a cluster
+            float bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            double pmax = 0.0;
+            const uint32_t slot0 = uint32_t(C.order.size());
+            for (uint32_t i = lo; i < hi; ++i) {
+                const float* v = V + 9 * size_t(first + idx[i]);
+                for (int c = 0; c < 3; ++c)
+                    for (int a = 0; a < 3; ++a) {
+                        bl[a] = std::min(bl[a], v[3 * c + a]);
+                        bh[a] = std::max(bh[a], v[3 * c + a]);
+                    }
+                // ab, ac exactly as the device holds them (f32 b - a, c - a)
+                double ab[3], ac[3];
+                for (int a = 0; a < 3; ++a) {
+                    ab[a] = double(v[3 + a] - v[a]);
+                    ac[a] = double(v[6 + a] - v[a]);
+                }
+                const double n[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2],
+                                     ab[0] * ac[1] - ab[1] * ac[0]};
+                pmax = std::max(pmax, std::sqrt(ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2]) *
+                                          std::sqrt(ac[0] * ac[0] + ac[1] * ac[1] + ac[2] * ac[2]));
+                // the culled test's det = ab . (d x ac) = -(d . n)
+                for (int a = 0; a < 3; ++a) C.normal.push_back(float(n[a]));
+                C.order.push_back(first + idx[i]);
+                C.rank.push_back(idx[i]);
+            }
+            // count (n - 1) rides in the low 5 mantissa bits of the |ab||ac| bound, rounded up
+            // first so the stored value is still an upper bound
+            float pf = float(pmax * (1.0 + 1e-5) + 1e-30);
+            uint32_t pb;
+            std::memcpy(&pb, &pf, 4);
+            pb = (pb & ~31u) + 32u;
+            pb |= (m - 1);
+            std::memcpy(&pf, &pb, 4);
+            float sf;
+            std::memcpy(&sf, &slot0, 4);
+            const float r[8] = {bl[0], bl[1], bl[2], pf, bh[0], bh[1], bh[2], sf};
+            C.rec.insert(C.rec.end(), r, r + 8);
+        }
+        C.range[2 * size_t(n) + 1] = uint32_t(C.rec.size() / 8) - C.range[2 * size_t(n)];
     }
     return ATR_OK;
 }

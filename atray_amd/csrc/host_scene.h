@@ -27,6 +27,19 @@ struct HostTree {
     std::vector<uint32_t> prim_face;
 };
 
+// Leaf clusters: each leaf's primitives regrouped into spatial clusters of <= `size` (median
+// splits on centroids), for the clustered leaf scan. Indices refer to the
+// tree's leaf-ordered primitives (prim_face / prim_vertices).
+struct LeafClusters {
+    std::vector<uint32_t> order;  // cluster-ordered slot -> leaf-ordered primitive index
+    std::vector<uint32_t> rank;   // slot -> rank of its primitive within its leaf
+    std::vector<float> rec;       // 8 per cluster (DModel::clus)
+    std::vector<float> normal;    // 3 per slot: ab x ac of its primitive
+    std::vector<uint32_t> range;  // 2 per node: first cluster, cluster count (leaves only)
+    float max_abs = 0.f;          // largest |coordinate| of any primitive vertex
+};
+int leaf_clusters(const HostTree& T, int size, LeafClusters& C);
+
 int parse_obj_text(const char* text, size_t len, HostMesh& m);
 void mesh_aabb(const HostMesh& m, float out[6]);
 void mesh_translate(HostMesh& m, float box[6], V3 c);

@@ -76,6 +76,113 @@ __device__ __forceinline__ bool scan_leaf_lane(const Ray& r, const DModel& m, ui
     return improved;
 }
 
+// ------------------------------------------------------------------ clustered leaf scan
+// The same leaf result from a fraction of the triangle tests. Each leaf's
+// primitives are regrouped into spatial clusters of <= 16 with a bounding box, and a primitive
+// is skipped only when it provably cannot be accepted with t <= the best so far:
+//   * rounding (first order): an accepted hit of the culled test (computed
+//     det >= kTol; u, v in range) has its true line within D_lat of the triangle and its
+//     computed t within D_t of the true t, D_lat + D_t <= W (29 eps |ab||ac| / det + 6 eps),
+//     W >= |o - a| + |edge|: the u, v, t numerators carry ~7.5 eps |tvec| |ac| (resp. |ab|,
+//     |ab||ac|) of cancellation, det ~6.5 eps |ab||ac|. A box grown by that much (36 and
+//     12 eps here, with the slab's own rounding) is entered no later than the computed t of any
+//     acceptable primitive inside and left no earlier.
+//   * D depends on det, which is not known per cluster: the box is grown twice, for det >= kTol
+//     (loose) and det >= kTau (tight). Missing the loose box skips the cluster. Inside the
+//     tight box every front-facing primitive is a candidate. In between, only primitives whose
+//     det could lie in [kTol, kTau) are: the det estimate -(d . n) (n = ab x ac, one 16-B
+//     load) is within 16 eps |ab||ac| of the computed det, which sets the screen's margins.
+//     Back-facing primitives (det < kTol) are screened out the same way in both cases.
+//   * inside the leaf the reference keeps the FIRST primitive (leaf order) with the smallest t
+//     below the incoming best (strict <, kd_tree.cpp:440-456); clusters change the visiting
+//     order, so equal t is resolved by the leaf rank, and a best carried in from an earlier
+//     leaf never loses a tie.
+constexpr float kTau = 3e-3f;
+constexpr float kEps = 5.9604645e-8f;  // 2^-24
+constexpr float kPadRel = 36.0f * kEps, kPadAbs = 12.0f * kEps;
+
+template <bool COUNT>
+__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, float acz, float& best_t,
+                                            uint32_t& best_slot, float& bu, float& bv, int32_t& brank,
+                                            bool& improved, Ctr& ct) {
+    if constexpr (COUNT) ct.tri += 1;
+    const float4_t q0 = m.c0[k], q1 = m.c1[k];
+    float u = 0.f, v = 0.f;
+    const float dist = tri_hit(r, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, acz), u, v);
+    if (dist <= best_t && dist > kTol) {
+        const int32_t rk = int32_t(m.crank[k]);
+        if (dist < best_t || (brank >= 0 && rk < brank)) {
+            best_t = dist;
+            best_slot = k;
+            bu = u;
+            bv = v;
+            brank = rk;
+            improved = true;
+        }
+    }
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m, uint32_t cfirst,
+                                                   uint32_t ccount, float& best_t, uint32_t& best_slot,
+                                                   float& bu, float& bv, Ctr& ct) {
+    if constexpr (COUNT) { ct.leaf += 1; ct.box_all += ccount; }
+    bool improved = false;
+    int32_t brank = -1;
+    const uint32_t cend = cfirst + ccount;
+    const float ax = fabsf(r.inv.x), ay = fabsf(r.inv.y), az = fabsf(r.inv.z);
+    float4_t nlo, nhi;  // next cluster's record, in flight while this one is screened
+    if (ccount) { nlo = m.clus[2 * cfirst]; nhi = m.clus[2 * cfirst + 1]; }
+    for (uint32_t c = cfirst; c < cend; ++c) {
+        const float4_t lo = nlo, hi = nhi;
+        if (c + 1 < cend) { nlo = m.clus[2 * c + 2]; nhi = m.clus[2 * c + 3]; }
+        const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
+        const float fx = fmaxf(fabsf(lo.x - r.o.x), fabsf(hi.x - r.o.x));
+        const float fy = fmaxf(fabsf(lo.y - r.o.y), fabsf(hi.y - r.o.y));
+        const float fz = fmaxf(fabsf(lo.z - r.o.z), fabsf(hi.z - r.o.z));
+        // W >= |o - a| + |edge| for every primitive inside (far corner; L1 extent >= diagonal)
+        const float W = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0000005f + (ex + ey + ez);
+        const float P = lo.w;  // >= |ab||ac| of every primitive inside
+        const float gl = W * (P * (kPadRel / (0.9f * kTol)) + kPadAbs);
+        const float gt = W * (P * (kPadRel / (0.9f * kTau)) + kPadAbs);
+        // slab entry/exit of the unpadded box per axis, then widened by g |inv| per axis
+        const float x0 = (lo.x - r.o.x) * r.inv.x, x1 = (hi.x - r.o.x) * r.inv.x;
+        const float y0 = (lo.y - r.o.y) * r.inv.y, y1 = (hi.y - r.o.y) * r.inv.y;
+        const float z0 = (lo.z - r.o.z) * r.inv.z, z1 = (hi.z - r.o.z) * r.inv.z;
+        const float nx = fminf(x0, x1), fx1 = fmaxf(x0, x1), ny = fminf(y0, y1), fy1 = fmaxf(y0, y1),
+                    nz = fminf(z0, z1), fz1 = fmaxf(z0, z1);
+        float tn = fmaxf(fmaxf(nx - gl * ax, ny - gl * ay), nz - gl * az);
+        float tf = fminf(fminf(fx1 + gl * ax, fy1 + gl * ay), fz1 + gl * az);
+        if (tn > tf || tf < 0.f || tn > best_t) continue;
+        tn = fmaxf(fmaxf(nx - gt * ax, ny - gt * ay), nz - gt * az);
+        tf = fminf(fminf(fx1 + gt * ax, fy1 + gt * ay), fz1 + gt * az);
+        const bool tight = !(tn > tf || tf < 0.f || tn > best_t);
+        const float mg = 16.0f * kEps * P;
+        const float dlo = kTol - mg, dhi = tight ? __builtin_inff() : kTau + mg;
+        const uint32_t first = __float_as_uint(hi.w);
+        const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u, last = first + n - 1;
+        if constexpr (COUNT) ct.wave_tri += n;
+        // screen four primitives per step (their normal loads in flight together)
+        for (uint32_t k = first; k <= last; k += 4) {
+            const uint32_t k1 = k + 1 <= last ? k + 1 : last, k2 = k + 2 <= last ? k + 2 : last,
+                           k3 = k + 3 <= last ? k + 3 : last;
+            const float4_t n0 = m.c2[k], n1 = m.c2[k1], n2 = m.c2[k2], n3 = m.c2[k3];
+            const float d0 = -(r.d.x * n0.x + r.d.y * n0.y + r.d.z * n0.z);
+            const float d1 = -(r.d.x * n1.x + r.d.y * n1.y + r.d.z * n1.z);
+            const float d2 = -(r.d.x * n2.x + r.d.y * n2.y + r.d.z * n2.z);
+            const float d3 = -(r.d.x * n3.x + r.d.y * n3.y + r.d.z * n3.z);
+            if (d0 >= dlo && d0 < dhi) cluster_tri<COUNT>(r, m, k, n0.w, best_t, best_slot, bu, bv, brank, improved, ct);
+            if (k + 1 <= last && d1 >= dlo && d1 < dhi)
+                cluster_tri<COUNT>(r, m, k + 1, n1.w, best_t, best_slot, bu, bv, brank, improved, ct);
+            if (k + 2 <= last && d2 >= dlo && d2 < dhi)
+                cluster_tri<COUNT>(r, m, k + 2, n2.w, best_t, best_slot, bu, bv, brank, improved, ct);
+            if (k + 3 <= last && d3 >= dlo && d3 < dhi)
+                cluster_tri<COUNT>(r, m, k + 3, n3.w, best_t, best_slot, bu, bv, brank, improved, ct);
+        }
+    }
+    return improved;
+}
+
 // Sorted-leaf scan with a rotating head: entry 0 is always the next leaf, the buffer shifts
 // down after each scanned leaf (static register moves, no dynamically indexed arrays).
 template <int K>
@@ -85,7 +192,7 @@ __device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
     b.d[K - 1] = __builtin_inff();
 }
 
-template <bool COUNT>
+template <bool COUNT, bool CL = false>
 __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m, Hit& h, int& err, Ctr& ct) {
     h.t = kMaxFloat;
     h.face = 0;
@@ -94,8 +201,15 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
     if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
     if (!box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) return;  // :339
     uint32_t slot = 0xFFFFFFFFu;
+    const uint32_t* range = CL ? m.cl_range : m.leaf_range;
+    auto scan = [&](int32_t leaf) -> bool {
+        if constexpr (CL)
+            return scan_leaf_clusters<COUNT>(r, m, range[2 * leaf], range[2 * leaf + 1], h.t, slot, h.u, h.v, ct);
+        else
+            return scan_leaf_lane<COUNT>(r, m, range[2 * leaf], range[2 * leaf + 1], h.t, slot, h.u, h.v, ct);
+    };
     if (root.children == 0) {  // :344-361
-        scan_leaf_lane<COUNT>(r, m, m.leaf_range[0], m.leaf_range[1], h.t, slot, h.u, h.v, ct);
+        scan(0);
     } else {
         float bd = -__builtin_inff();
         int32_t bi = -1;
@@ -111,15 +225,14 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
                 const int32_t leaf = lb.node[0];
                 bd = lb.d[0];
                 bi = lb.idx[0];
-                if (scan_leaf_lane<COUNT>(r, m, m.leaf_range[2 * leaf], m.leaf_range[2 * leaf + 1], h.t, slot,
-                                          h.u, h.v, ct)) { hit = true; break; }
+                if (scan(leaf)) { hit = true; break; }
                 lb_pop<kLeafBuf>(lb);
                 --nb;
             }
             if (hit) break;
         }
     }
-    if (slot != 0xFFFFFFFFu) h.face = m.tface[slot];
+    if (slot != 0xFFFFFFFFu) h.face = CL ? m.cface[slot] : m.tface[slot];
 }
 
 // ------------------------------------------------------------------ WAVE schedule
@@ -359,9 +472,9 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 }
 
 // ------------------------------------------------------------------ get_intersection_data
-enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3 };
+enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4 };
 constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
-constexpr bool sched_coop(int sc) { return sc != SCHED_LANE; }  // lanes must stay in lockstep loops
+constexpr bool sched_coop(int sc) { return sc != SCHED_LANE && sc != SCHED_CLUSTER; }  // lanes must stay in lockstep loops
 
 template <int SCHED, bool COUNT>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
@@ -379,6 +492,10 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
+            else if constexpr (SCHED == SCHED_CLUSTER) {
+                if (active) tree_closest_lane<COUNT, true>(r, m, h, err, ct);
+                else h.t = kMaxFloat;
+            }
             else if (active) tree_closest_lane<COUNT>(r, m, h, err, ct);
             else h.t = kMaxFloat;
             if (h.t > kTol && h.t < best) { best = h.t; face = h.face; fu = h.u; fv = h.v; nm = i; }
@@ -611,12 +728,15 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
 
 #define ATR_INST(SC, C, PR) template __global__ void render_kernel<SC, C, PR>(RenderParams);
 #define ATR_INST4(SC) ATR_INST(SC, false, false) ATR_INST(SC, true, false) ATR_INST(SC, false, true) ATR_INST(SC, true, true)
-ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCHED_TILE8)
+ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCHED_TILE8) ATR_INST4(SCHED_CLUSTER)
 #undef ATR_INST4
 #undef ATR_INST
 template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_LANE, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_LANE, false, true, 8>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER, false, true, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER, false, true, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER, false, true, 8>(RenderParams);
 
 __global__ __launch_bounds__(256) void unpack_kernel(const DBlock* __restrict__ blocks, int32_t nblocks,
                                                      int32_t width, const uint32_t* __restrict__ packed,
@@ -655,6 +775,7 @@ __global__ __launch_bounds__(256) void tile_casts_kernel(const atr_tile* __restr
 // launchers used by capi.cpp
 // Default occupancy of the PRIMARY lane kernel (waves/SIMD; chosen by measurement).
 constexpr int kPrimaryOcc = 5;
+constexpr int kClusterOcc = 5;
 
 template <int SC, bool C, bool PR>
 static void launch_one(const atr::RenderParams& P, hipStream_t s) {
@@ -669,12 +790,20 @@ static void launch_sched(const atr::RenderParams& P, bool count, bool prim, hipS
     else { if (prim) launch_one<SC, false, true>(P, s); else launch_one<SC, false, false>(P, s); }
 }
 
-// sched: 0 LANE, 1 WAVE, 2 TILE4, 3 TILE8; 16 + n: LANE at n waves/SIMD (diagnostic)
+// sched: 0 LANE, 1 WAVE, 2 TILE4, 3 TILE8, 4 CLUSTER; 16 + n: LANE at n waves/SIMD (diagnostic)
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, hipStream_t s) {
     if (P.nblocks <= 0) return hipSuccess;
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);
+    if (sched >= 32) {  // CLUSTER at 32 + n waves/SIMD (diagnostic)
+        const int o = sched - 32;
+        if (prim && !count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER, false, true, 5>), g, b, 0, s, P);
+        else if (prim && !count && o == 6) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER, false, true, 6>), g, b, 0, s, P);
+        else if (prim && !count && o == 8) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER, false, true, 8>), g, b, 0, s, P);
+        else launch_sched<atr::SCHED_CLUSTER>(P, count, prim, s);
+        return hipGetLastError();
+    }
     int occ = sched >= 16 ? sched - 16 : (sched == 0 ? kPrimaryOcc : 0);
     if (sched >= 16) sched = 0;
     if (sched == 0 && prim && !count && occ != 4) {
@@ -687,6 +816,10 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
         case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;
         case 3: launch_sched<atr::SCHED_TILE8>(P, count, prim, s); break;
+        case 4:
+            if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER, false, true, kClusterOcc>), g, b, 0, s, P);
+            else launch_sched<atr::SCHED_CLUSTER>(P, count, prim, s);
+            break;
         default: launch_sched<atr::SCHED_LANE>(P, count, prim, s); break;
     }
     return hipGetLastError();

@@ -1,0 +1,77 @@
+"""GPU parity of the clustered leaf scan (ATR_KERNEL_CLUSTER) on inputs built to
+break it: near-grazing triangles whose det sits just above the culling tolerance (where the
+rounding bound of the cluster test is widest), back-facing copies, and exact duplicates of
+triangles (equal t, so the reference's leaf-order tie rule decides). Every pixel's face index
+and t bits must equal the oracle's restatement of the reference traversal."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from atray_amd import engine as E  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from tests.goldens import SEED  # noqa: E402
+from tests.test_gpu_parity import MODEL, SKY, eng, run  # noqa: E402,F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _unit(v):
+    return v / np.linalg.norm(v, axis=-1, keepdims=True)
+
+
+def grazing_soup(n, seed, det=(1.0, 4.0), size=0.4, dup_every=5):
+    """OBJ text: n triangles around camera rays, each tilted off the ray through it just enough
+    that the culled test's det = |n| sin(tilt) is det[0]..det[1] times its tolerance (1e-4)."""
+    rng = np.random.default_rng(seed)
+    cm = E.camera(64, 64)
+    v = lambda a: np.array([a.x, a.y, a.z], np.float64)  # noqa: E731
+    eye, fc, cx, cy = v(cm.eye), v(cm.frame_center), v(cm.camera_x), v(cm.camera_y)
+    fx = rng.uniform(-0.9, 0.9, n) * cm.h_fov * cm.aspect_ratio
+    fy = rng.uniform(-0.9, 0.9, n)
+    d = _unit(fc[None] + fx[:, None] * cx[None] + fy[:, None] * cy[None] - eye[None])
+    p = eye[None] + d * rng.uniform(2.0, 9.0, n)[:, None]
+    u = _unit(np.cross(d, rng.normal(size=(n, 3))))
+    w = _unit(np.cross(d, u))                       # d, u, w orthonormal
+    s = size * rng.uniform(0.3, 1.0, (n, 3))
+    area2 = (s[:, 0] * 2) * (s[:, 1] * 2 + s[:, 2]) / 2 + 1e-12   # |ab x ac| at zero tilt (approx.)
+    sin_t = np.clip(1e-4 * rng.uniform(*det, n) / area2, 0.0, 1.0)
+    ang = np.arcsin(sin_t) * rng.choice([-1.0, 1.0], n)
+    dp = d * np.cos(ang)[:, None] + w * np.sin(ang)[:, None]   # in-plane axis, tilted off d
+    a = p - dp * s[:, :1] - u * s[:, 1:2]
+    b = p + dp * s[:, :1] - u * s[:, 2:3]
+    c = p + u * s[:, 1:2]
+    flip = rng.random(n) < 0.5                      # half wound the other way (back-facing)
+    b2 = np.where(flip[:, None], c, b)
+    c2 = np.where(flip[:, None], b, c)
+    tris = np.stack([a, b2, c2], 1)
+    # exact duplicates, some adjacent in face order and some far away
+    dups = tris[::dup_every]
+    tris = np.concatenate([tris[:n // 2], dups[: len(dups) // 2], tris[n // 2:], dups[len(dups) // 2:],
+                           dups[::3]])
+    lines = []
+    for t in tris:
+        for q in t:
+            lines.append("v %.6f %.6f %.6f" % tuple(q))
+    for i in range(len(tris)):
+        lines.append("f %d %d %d" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("seed,n,det,leaf", [(1, 12000, (1.0, 4.0), 300), (2, 12000, (0.5, 2.0), 300),
+                                             (3, 12000, (1.0, 100.0), 64), (4, 6000, (20.0, 2000.0), 300)])
+def test_cluster_scan_bit_exact_on_grazing_soup(eng, seed, n, det, leaf):
+    txt = grazing_soup(n, seed, det)
+    W, H = 512, 384
+    cam = E.camera(W, H)
+    s = O.Scene(obj_text=txt, center=None, max_faces=leaf, use_tree=True)
+    face_o, t_o, _ = s.primary_hits(O.Camera(W, H))
+    m = E.Mesh.parse_obj(txt)
+    tree = E.Octree.build(m, leaf)
+    eng.upload([SKY, MODEL], [(m, tree, m.aabb(), 1)], (), ())
+    hit = face_o != 0xFFFFFFFF
+    assert hit.sum() > 1000, hit.sum()   # the soup must actually be hit
+    for variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_LANE):
+        o = run(eng, cam, variant=variant)
+        bad = np.argwhere((o["face"] != face_o) | (o["t"].view(np.uint32) != t_o.view(np.uint32)))
+        assert len(bad) == 0, (variant, len(bad), bad[:5].tolist())
