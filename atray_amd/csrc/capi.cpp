@@ -771,7 +771,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
 }
 
 int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                        uint64_t seed, int32_t variant, int64_t out[8]) {
+                        uint64_t seed, int32_t variant, int64_t out[10]) {
     if (!c || !cam || !out || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
@@ -781,8 +781,8 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     void* fb = nullptr;
     void* ctr = nullptr;
     HIPCHK(hipMalloc(&fb, size_t(cam->width) * size_t(cam->height) * 4));
-    HIPCHK(hipMalloc(&ctr, 8 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(ctr, 0, 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&ctr, 10 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctr, 0, 10 * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -794,11 +794,12 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.framebuffer = static_cast<uint32_t*>(fb);
     P.error_flag = c->d_error;
     P.counters = static_cast<unsigned long long*>(ctr);
-    HIPCHK(atr_launch_render(P, sched_of(variant) >= 16 ? 0 : sched_of(variant), nullptr));
+    const int sc = sched_of(variant);
+    HIPCHK(atr_launch_render(P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
-    unsigned long long h[8];
+    unsigned long long h[10];
     HIPCHK(hipMemcpy(h, ctr, sizeof(h), hipMemcpyDeviceToHost));
-    for (int k = 0; k < 8; ++k) out[k] = int64_t(h[k]);
+    for (int k = 0; k < 10; ++k) out[k] = int64_t(h[k]);
     HIPCHK(hipFree(fb));
     HIPCHK(hipFree(ctr));
     return ATR_OK;

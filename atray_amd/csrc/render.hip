@@ -126,7 +126,7 @@ template <bool COUNT>
 __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m, uint32_t cfirst,
                                                    uint32_t ccount, float& best_t, uint32_t& best_slot,
                                                    float& bu, float& bv, Ctr& ct) {
-    if constexpr (COUNT) { ct.leaf += 1; ct.box_all += ccount; }
+    if constexpr (COUNT) { ct.leaf += 1; ct.cbox += ccount; }
     bool improved = false;
     int32_t brank = -1;
     const uint32_t cend = cfirst + ccount;
@@ -161,7 +161,7 @@ __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m
         const float dlo = kTol - mg, dhi = tight ? __builtin_inff() : kTau + mg;
         const uint32_t first = __float_as_uint(hi.w);
         const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u, last = first + n - 1;
-        if constexpr (COUNT) ct.wave_tri += n;
+        if constexpr (COUNT) ct.screen += n;
         // screen four primitives per step (their normal loads in flight together)
         for (uint32_t k = first; k <= last; k += 4) {
             const uint32_t k1 = k + 1 <= last ? k + 1 : last, k2 = k + 2 <= last ? k + 2 : last,
@@ -192,7 +192,7 @@ __device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
     b.d[K - 1] = __builtin_inff();
 }
 
-template <bool COUNT, bool CL = false>
+template <bool COUNT, bool CL = false, int K = kLeafBuf>
 __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m, Hit& h, int& err, Ctr& ct) {
     h.t = kMaxFloat;
     h.face = 0;
@@ -215,18 +215,18 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
         int32_t bi = -1;
         bool more = true;
         while (more) {
-            LeafBuf<kLeafBuf> lb;
-            const int32_t n = traverse_pass<kLeafBuf, COUNT>(r, m.nodes, lb, bd, bi, ct);
+            LeafBuf<K> lb;
+            const int32_t n = traverse_pass<K, COUNT>(r, m.nodes, lb, bd, bi, ct);
             if (n < 0) { err = 1; break; }
-            int32_t nb = n < kLeafBuf ? n : kLeafBuf;
-            more = n > kLeafBuf;
+            int32_t nb = n < K ? n : K;
+            more = n > K;
             bool hit = false;
             while (nb > 0) {
                 const int32_t leaf = lb.node[0];
                 bd = lb.d[0];
                 bi = lb.idx[0];
                 if (scan(leaf)) { hit = true; break; }
-                lb_pop<kLeafBuf>(lb);
+                lb_pop<K>(lb);
                 --nb;
             }
             if (hit) break;
@@ -472,9 +472,9 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 }
 
 // ------------------------------------------------------------------ get_intersection_data
-enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4 };
+enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5 };
 constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
-constexpr bool sched_coop(int sc) { return sc != SCHED_LANE && sc != SCHED_CLUSTER; }  // lanes must stay in lockstep loops
+constexpr bool sched_coop(int sc) { return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4; }  // lanes must stay in lockstep loops
 
 template <int SCHED, bool COUNT>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
@@ -494,6 +494,10 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
                 if (active) tree_closest_lane<COUNT, true>(r, m, h, err, ct);
+                else h.t = kMaxFloat;
+            }
+            else if constexpr (SCHED == SCHED_CLUSTER_K4) {  // 4-entry leaf buffer (fewer VGPRs)
+                if (active) tree_closest_lane<COUNT, true, 4>(r, m, h, err, ct);
                 else h.t = kMaxFloat;
             }
             else if (active) tree_closest_lane<COUNT>(r, m, h, err, ct);
@@ -709,7 +713,8 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     }
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
     if constexpr (COUNT) {
-        // counters[0..7]: rays, box(ref), tri, leaf, wave_tri_iters, passes, box_all, waves
+        // counters[0..9]: rays, box(ref), tri, leaf, wave_tri_iters, passes, box_all, waves,
+        // cluster boxes, screened primitives
         uint32_t v[6] = {ct.box, ct.tri, ct.leaf, ct.wave_tri, ct.pass, ct.box_all};
         unsigned long long* C = P.counters;
 #pragma unroll
@@ -723,6 +728,14 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
         if (lane == 0) { atomicAdd(C + 0, (unsigned long long)t); if (in_range) atomicAdd(C + 7, 1ull); }
+        uint32_t w[2] = {ct.cbox, ct.screen};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            uint32_t x = w[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+            if (lane == 0 && x) atomicAdd(C + 8 + k, (unsigned long long)x);
+        }
     }
 }
 
@@ -737,6 +750,10 @@ template __global__ void render_kernel<SCHED_LANE, false, true, 8>(RenderParams)
 template __global__ void render_kernel<SCHED_CLUSTER, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_CLUSTER, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_CLUSTER, false, true, 8>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 4>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 8>(RenderParams);
 
 __global__ __launch_bounds__(256) void unpack_kernel(const DBlock* __restrict__ blocks, int32_t nblocks,
                                                      int32_t width, const uint32_t* __restrict__ packed,
@@ -796,6 +813,15 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);
+    if (sched >= 48) {  // CLUSTER with a 4-entry leaf buffer at 48 + n waves/SIMD (diagnostic)
+        const int o = sched - 48;
+        if (!prim || count) return hipErrorInvalidValue;
+        if (o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER_K4, false, true, 5>), g, b, 0, s, P);
+        else if (o == 6) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER_K4, false, true, 6>), g, b, 0, s, P);
+        else if (o == 8) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER_K4, false, true, 8>), g, b, 0, s, P);
+        else hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER_K4, false, true, 4>), g, b, 0, s, P);
+        return hipGetLastError();
+    }
     if (sched >= 32) {  // CLUSTER at 32 + n waves/SIMD (diagnostic)
         const int o = sched - 32;
         if (prim && !count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_CLUSTER, false, true, 5>), g, b, 0, s, P);

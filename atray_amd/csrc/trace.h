@@ -20,6 +20,7 @@ namespace atr {
 // the engine's own extra work (re-walk passes, all box tests, wave-level triangle iterations).
 struct Ctr {
     uint32_t box = 0, box_all = 0, tri = 0, leaf = 0, wave_tri = 0, pass = 0;
+    uint32_t cbox = 0, screen = 0;  // clustered scan: cluster boxes tested, primitives screened
 };
 
 struct Ray {

@@ -132,7 +132,7 @@ def lib():
         "atr_render_start": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp], C.c_int),
         "atr_render_start_ex": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32], C.c_int),
         "atr_render_packed_size": ([vp, i32], i64),
-        "atr_render_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, i64 * 8], C.c_int),
+        "atr_render_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, i64 * 10], C.c_int),
         "atr_packed_pixel_map": ([vp, i32, i32, i32, vp, i64], i64),
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
@@ -147,8 +147,19 @@ def lib():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    global _sig
+    _sig = sig
     _lib = L
     return L
+
+
+_sig = None
+
+
+def signatures():
+    """{symbol: (argtypes, restype)} of the ctypes binding."""
+    lib()
+    return dict(_sig)
 
 
 def vec3(t):
@@ -326,10 +337,11 @@ class Engine:
 
     def counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
         arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
-        out = (C.c_int64 * 8)()
+        out = (C.c_int64 * 10)()
         check(lib().atr_render_counters(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n,
                                         C.c_uint64(seed & (2**64 - 1)), int(variant), out), "counters")
-        keys = ["n_rays", "n_box", "n_tri", "n_leaf", "wave_tri_iters", "passes", "box_all", "waves"]
+        keys = ["n_rays", "n_box", "n_tri", "n_leaf", "wave_tri_iters", "passes", "box_all", "waves",
+                "cluster_boxes", "screened"]
         return dict(zip(keys, [int(x) for x in out]))
 
     def wait(self, timeout_ms=0xFFFFFFFF):

@@ -46,6 +46,16 @@ def algorithmic_bytes_per_ray(ctr):
     return (36.0 + 28.0 * ctr["n_box"] / n + 40.0 * ctr["n_tri"] / n + 8.0 * ctr["n_leaf"] / n)
 
 
+def cluster_bytes_per_ray(ctr):
+    """The clustered scan's own algorithmic bytes: ray in + hit out (36), the
+    reference traversal's box tests (28 each) and leaf records (8), cluster records (32), one
+    16-B normal+ac.z per screened primitive, 32 B more (a, ab, ac.xy) per full triangle test.
+    N_* counted live by the instrumented build of the same kernel on the same frame."""
+    n = ctr["n_rays"]
+    return (36.0 + 28.0 * ctr["n_box"] / n + 8.0 * ctr["n_leaf"] / n + 32.0 * ctr["cluster_boxes"] / n
+            + 16.0 * ctr["screened"] / n + 32.0 * ctr["n_tri"] / n)
+
+
 def pmc_traffic(args, kernel_name="render_kernel"):
     """HBM bytes per render launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a
     short child run of this benchmark. FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950
@@ -196,6 +206,9 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     rc, _ = eng.wait()
     assert rc == 0
+    # the dominant kernel's work on this rank's tiles, counted by the instrumented build of the
+    # same variant (untimed; deterministic)
+    live_ctr = eng.counters(cam, tiles, SEED, variant) if rank == 0 else None
 
     if rank == 0:
         value = rays_per_step * args.steps / elapsed / 1e6
@@ -210,15 +223,23 @@ def main():
                           "parallelism": f"tiles{world}", "kernel": args.variant}}
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
+        clustered = args.variant in ("auto", "cl")
+        if clustered:
+            bpr = cluster_bytes_per_ray(live_ctr)
+        else:
+            bpr = algorithmic_bytes_per_ray(live_ctr)
+        achieved = bpr * live_ctr["n_rays"] / (kern_ms * 1e-3) / 1e9
+        roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "bytes_per_ray": round(bpr, 1), "rays_per_launch": live_ctr["n_rays"],
+                     "model": "clustered scan, own work (DESIGN.md 6)" if clustered
+                     else "reference work (SURVEY.md 8(d))"})
         gname = GOLDEN_COUNTERS.get(args.config)
-        if gname:
+        if gname:  # the reference algorithm's bytes for the same rays, at this kernel's speed
             with open(os.path.join(ROOT, "tests", "golden", "goldens.json")) as f:
                 ctr = json.load(f)["hits"][gname]["counters"]
-            bpr = algorithmic_bytes_per_ray(ctr)
-            rays_launch = W * H * spp if world == 1 else sizes[0] * spp
-            achieved = bpr * rays_launch / (kern_ms * 1e-3) / 1e9
-            roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "bytes_per_ray": round(bpr, 1), "rays_per_launch": rays_launch})
+            rbpr = algorithmic_bytes_per_ray(ctr)
+            roof["ref_bytes_per_ray"] = round(rbpr, 1)
+            roof["ref_equivalent_GBs"] = round(rbpr * live_ctr["n_rays"] / (kern_ms * 1e-3) / 1e9, 1)
         if world == 1 and not args.no_pmc:
             traffic, why = pmc_traffic(args)
             roof["traffic"] = traffic

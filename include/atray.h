@@ -159,10 +159,12 @@ int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
                         const atr_frame* frame, uint64_t seed, void* stream, int32_t variant);
 /* Diagnostic, synchronous: an instrumented render of the same work that returns
    [0] traced rays, [1] box tests, [2] triangle tests, [3] leaves scanned -- the reference's own
-   per-ray work on this input (kd_tree.cpp:337-465) -- and the engine's [4] wave-level triangle
-   iterations, [5] DFS passes, [6] all box tests, [7] wavefronts. */
+   per-ray work on this input (kd_tree.cpp:337-465) for every variant but CLUSTER, whose [2]
+   counts the full triangle tests it still runs -- and the engine's [4] wave-level triangle
+   iterations, [5] DFS passes, [6] all octree box tests, [7] wavefronts, [8] cluster boxes tested
+   and [9] primitives screened by the clustered scan. */
 int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                        uint64_t seed, int32_t variant, int64_t counters_out[8]);
+                        uint64_t seed, int32_t variant, int64_t counters_out[10]);
 /* Number of pixels a PACKED render of these tiles writes. */
 int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles);
 /* Host-only: pixel index (y * width + x) of every slot of a PACKED render of these tiles, in

@@ -31,6 +31,24 @@ def test_library_exports_every_declared_symbol():
     assert b"gfx950" in L.atr_version()
 
 
+def test_ctypes_fixed_arrays_match_header():
+    """Every fixed-size array parameter of a prototype (e.g. counters_out[10]) has the same
+    length in the ctypes signature table, so no call can under-allocate an output."""
+    txt = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    sig = E.signatures()
+    checked = 0
+    for name, params in re.findall(r"\b(atr_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", txt):
+        for i, p in enumerate(x.strip() for x in params.split(",")):
+            m = re.search(r"\[(\d+)\]$", p)
+            if not m or name not in sig:
+                continue
+            at = sig[name][0][i]
+            if isinstance(at, type) and issubclass(at, C.Array):
+                assert at._length_ == int(m.group(1)), (name, p, at._length_)
+                checked += 1
+    assert checked >= 1
+
+
 def _engine_tree(asset, leaf=300):
     m = E.Mesh.load_obj(asset_path(asset))
     box = m.aabb()

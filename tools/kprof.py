@@ -45,7 +45,8 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     names = {"lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE, "tile": E.ATR_KERNEL_TILE,
              "tile8": E.ATR_KERNEL_TILE8, "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER, "occ4": 20, "occ5": 21,
-             "occ6": 22, "occ8": 24, "cl4": 36, "cl5": 37, "cl6": 38, "cl8": 40}
+             "occ6": 22, "occ8": 24, "cl4": 36, "cl5": 37, "cl6": 38, "cl8": 40,
+             "k4o4": 52, "k4o5": 53, "k4o6": 54, "k4o8": 56}
     vs = args.variants.split(",")
     res = {v: [] for v in vs}
     ctrs = {v: eng.counters(cam, tiles, SEED, names[v] if names[v] in (1, 2, 3, 4, 6) else (E.ATR_KERNEL_CLUSTER if names[v] >= 32 else E.ATR_KERNEL_LANE)) for v in vs}
