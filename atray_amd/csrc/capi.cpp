@@ -421,6 +421,11 @@ int32_t atr_make_shard_tiles(int32_t w, int32_t h, int32_t side, int32_t rank, i
     return shard_tiles(w, h, side, rank, world, out, out ? cap : 0);
 }
 
+int32_t atr_balance_shard_tiles(int32_t w, int32_t h, int32_t side, int32_t world, const int64_t* costs,
+                                int64_t rank0_extra, int32_t* owner_out) {
+    return balance_shard_tiles(w, h, side, world, costs, rank0_extra, owner_out);
+}
+
 // ------------------------------------------------------------------ device engine
 int atr_create(int device, atr_ctx** out) {
     if (!out) return ATR_E_INVALID;
@@ -802,6 +807,52 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     for (int k = 0; k < 10; ++k) out[k] = int64_t(h[k]);
     HIPCHK(hipFree(fb));
     HIPCHK(hipFree(ctr));
+    return ATR_OK;
+}
+
+int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                          uint64_t seed, int64_t* cost_out) {
+    if (!c || !cam || (ntiles && (!tiles || !cost_out)) || ntiles < 0) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
+    if (!bs) return rc;
+    const size_t nb = bs->host.size();
+    void* fb = nullptr;
+    void* cost = nullptr;
+    HIPCHK(hipMalloc(&fb, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
+    HIPCHK(hipMalloc(&cost, std::max<size_t>(1, nb) * sizeof(unsigned long long)));
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.blocks = static_cast<const DBlock*>(bs->dev.p);
+    P.nblocks = int32_t(nb);
+    P.layout = ATR_LAYOUT_PACKED;
+    P.framebuffer = static_cast<uint32_t*>(fb);
+    P.error_flag = c->d_error;
+    P.block_cost = static_cast<unsigned long long*>(cost);
+    HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_AUTO), nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(nb);
+    if (nb) HIPCHK(hipMemcpy(h.data(), cost, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(fb));
+    HIPCHK(hipFree(cost));
+    // a block belongs to the first tile (list order) that holds its origin pixel
+    for (int32_t t = 0; t < ntiles; ++t) cost_out[t] = 0;
+    for (size_t k = 0; k < nb; ++k) {
+        const DBlock& b = bs->host[k];
+        for (int32_t t = 0; t < ntiles; ++t) {
+            const atr_tile& T = tiles[t];
+            const int32_t x = std::max(b.x0, T.min_x), y = std::max(b.y0, T.min_y);
+            if (x <= T.max_x && y <= T.max_y && x < b.x0 + 8 && y < b.y0 + 8) {
+                cost_out[t] += int64_t(h[k]);
+                break;
+            }
+        }
+    }
     return ATR_OK;
 }
 

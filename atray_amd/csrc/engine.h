@@ -156,7 +156,8 @@ struct RenderParams {
     uint32_t* ray_casts;
     unsigned long long* traced_rays;
     int32_t* error_flag;  // set to 1 if a ray hit a traversal limit (never for depth <= 16)
-    unsigned long long* counters;  // non-null -> instrumented kernel (8 u64, see render.hip)
+    unsigned long long* counters;  // non-null -> instrumented kernel (10 u64, see render.hip)
+    unsigned long long* block_cost;  // non-null -> shader clocks spent per block (load balance)
 };
 
 }  // namespace atr

@@ -462,3 +462,25 @@ int32_t atr::shard_tiles(int32_t W, int32_t H, int32_t side, int32_t rank, int32
         }
     return n;
 }
+
+// Longest-processing-time-first deal of the shard grid (side x side tiles, row-major) to
+// `world` ranks by measured cost: tiles in descending cost (ties: grid order) go to the least
+// loaded rank (ties: lowest rank); rank 0 starts with `rank0_extra` (its frame assembly work).
+int32_t atr::balance_shard_tiles(int32_t W, int32_t H, int32_t side, int32_t world, const int64_t* costs,
+                                 int64_t rank0_extra, int32_t* owner) {
+    if (W <= 0 || H <= 0 || side <= 0 || world <= 0 || !costs || !owner) return -1;
+    const int32_t nx = (W + side - 1) / side, ny = (H + side - 1) / side, n = nx * ny;
+    std::vector<int32_t> order(static_cast<size_t>(n));
+    for (int32_t i = 0; i < n; ++i) order[size_t(i)] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return costs[a] > costs[b]; });
+    std::vector<int64_t> load(size_t(world), 0);
+    load[0] = rank0_extra;
+    for (int32_t i : order) {
+        int32_t best = 0;
+        for (int32_t r = 1; r < world; ++r)
+            if (load[size_t(r)] < load[size_t(best)]) best = r;
+        owner[i] = best;
+        load[size_t(best)] += costs[i];
+    }
+    return n;
+}

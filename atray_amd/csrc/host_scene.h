@@ -49,6 +49,8 @@ void octree_stats(const HostTree& T, int64_t s[7]);
 void camera_set(atr_camera& cm, V3 eye, V3 facing, int32_t w, int32_t h, int32_t aa, uint32_t spp,
                 int32_t bounces, float h_fov);
 int32_t reference_tiles(int32_t W, int32_t H, int32_t threads, atr_tile* out, int32_t cap);
+int32_t balance_shard_tiles(int32_t W, int32_t H, int32_t side, int32_t world, const int64_t* costs,
+                            int64_t rank0_extra, int32_t* owner);
 int32_t shard_tiles(int32_t W, int32_t H, int32_t side, int32_t rank, int32_t world, atr_tile* out,
                     int32_t cap);
 

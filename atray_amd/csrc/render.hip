@@ -649,6 +649,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
     const bool active = (mask >> lane) & 1;
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
+    const uint64_t clk0 = P.block_cost ? clock64() : 0;
     const atr_camera& cm = P.cam;
     const DScene* S = P.scene;
     int err = 0;
@@ -712,6 +713,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         if (lane == 0 && t) atomicAdd(P.traced_rays, (unsigned long long)t);
     }
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
+    if (P.block_cost && lane == 0 && in_range) P.block_cost[b] = clock64() - clk0;
     if constexpr (COUNT) {
         // counters[0..9]: rays, box(ref), tri, leaf, wave_tri_iters, passes, box_all, waves,
         // cluster boxes, screened primitives

@@ -88,7 +88,7 @@ EXPORTS = [
     "atr_octree_from_nodes", "atr_octree_free", "atr_octree_export", "atr_octree_stats", "atr_camera_set",
     "atr_make_tiles", "atr_make_shard_tiles", "atr_create", "atr_destroy", "atr_version",
     "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
-    "atr_render_counters",
+    "atr_render_counters", "atr_render_tile_costs", "atr_balance_shard_tiles",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d",
@@ -124,6 +124,7 @@ def lib():
         "atr_camera_set": ([P(atr_camera), atr_vec3, atr_vec3, i32, i32, i32, u32, i32, C.c_float], C.c_int),
         "atr_make_tiles": ([i32, i32, i32, vp, i32], i32),
         "atr_make_shard_tiles": ([i32, i32, i32, i32, i32, vp, i32], i32),
+        "atr_balance_shard_tiles": ([i32, i32, i32, i32, vp, i64, vp], i32),
         "atr_create": ([C.c_int, P(vp)], C.c_int),
         "atr_destroy": ([vp], C.c_int),
         "atr_version": ([], C.c_char_p),
@@ -133,6 +134,7 @@ def lib():
         "atr_render_start_ex": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32], C.c_int),
         "atr_render_packed_size": ([vp, i32], i64),
         "atr_render_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, i64 * 10], C.c_int),
+        "atr_render_tile_costs": ([vp, P(atr_camera), vp, i32, C.c_uint64, vp], C.c_int),
         "atr_packed_pixel_map": ([vp, i32, i32, i32, vp, i64], i64),
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
@@ -181,6 +183,26 @@ def make_tiles(width, height, threads):
     buf = (atr_tile * max(1, n))()
     L.atr_make_tiles(width, height, threads, C.cast(buf, C.c_void_p), n)
     return np.array([[t.min_x, t.min_y, t.max_x, t.max_y] for t in buf[:n]], np.int32).reshape(-1, 4)
+
+
+def shard_grid(width, height, side):
+    """The side x side shard grid, row-major, as an (n, 4) array of inclusive rects."""
+    t = []
+    for y in range(0, height, side):
+        for x in range(0, width, side):
+            t.append([x, y, min(x + side, width) - 1, min(y + side, height) - 1])
+    return np.array(t, np.int32).reshape(-1, 4)
+
+
+def balance_shard_tiles(width, height, side, world, costs, rank0_extra=0):
+    """Owner rank per grid tile, longest-processing-time-first by measured cost."""
+    costs = np.ascontiguousarray(costs, np.int64)
+    owner = np.zeros(len(costs), np.int32)
+    n = lib().atr_balance_shard_tiles(width, height, side, world, costs.ctypes.data, int(rank0_extra),
+                                      owner.ctypes.data)
+    if n != len(costs):
+        raise AtrError(f"atr_balance_shard_tiles: {n} tiles for {len(costs)} costs")
+    return owner
 
 
 def make_shard_tiles(width, height, side, rank, world):
@@ -343,6 +365,14 @@ class Engine:
         keys = ["n_rays", "n_box", "n_tri", "n_leaf", "wave_tri_iters", "passes", "box_all", "waves",
                 "cluster_boxes", "screened"]
         return dict(zip(keys, [int(x) for x in out]))
+
+    def tile_costs(self, cam, tiles, seed):
+        """Shader clocks spent per tile by one render of `tiles` (load-balance calibration)."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        out = np.zeros(max(1, n), np.int64)
+        check(lib().atr_render_tile_costs(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n,
+                                          C.c_uint64(seed & (2**64 - 1)), out.ctypes.data), "tile costs")
+        return out[:n]
 
     def wait(self, timeout_ms=0xFFFFFFFF):
         done = C.c_int32()

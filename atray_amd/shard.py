@@ -16,14 +16,46 @@ from . import engine as E
 
 
 class ShardPlan:
-    def __init__(self, width: int, height: int, world: int, side: int = 64):
+    """Which side x side tiles each rank traces. Default: round-robin deal of the row-major grid
+    (atr_make_shard_tiles). With `owner` (one rank per grid tile, e.g. from `balanced`): that
+    assignment, each rank's tiles kept in grid order."""
+
+    def __init__(self, width: int, height: int, world: int, side: int = 64, owner=None):
         self.width, self.height, self.world, self.side = width, height, world, side
-        self.tiles = [E.make_shard_tiles(width, height, side, r, world) for r in range(world)]
+        if owner is None:
+            self.tiles = [E.make_shard_tiles(width, height, side, r, world) for r in range(world)]
+        else:
+            grid = E.shard_grid(width, height, side)
+            owner = np.asarray(owner, np.int32)
+            assert len(owner) == len(grid) and owner.min() >= 0 and owner.max() < world
+            self.tiles = [grid[owner == r] for r in range(world)]
+        self.owner = owner
         self.sizes = [E.packed_size(t) if len(t) else 0 for t in self.tiles]
         self.max_size = max(1, max(self.sizes))
 
+    @classmethod
+    def balanced(cls, costs, width: int, height: int, world: int, side: int = 64, rank0_extra: float = 0.0):
+        """Longest-first deal by measured per-tile cost (`tile_costs`); rank 0 starts with
+        rank0_extra x the mean per-rank load (its frame assembly)."""
+        costs = np.asarray(costs, np.int64)
+        extra = int(rank0_extra * costs.sum() / max(1, world))
+        return cls(width, height, world, side, E.balance_shard_tiles(width, height, side, world, costs, extra))
+
     def pixel_map(self, rank: int) -> np.ndarray:
         return E.packed_pixel_map(self.tiles[rank], self.width, self.height)
+
+
+def tile_costs(eng, cam, width: int, height: int, side: int, seed: int) -> np.ndarray:
+    """Measured cost (GPU shader clocks) of every grid tile: one calibration render."""
+    return eng.tile_costs(cam, E.shard_grid(width, height, side), seed)
+
+
+def shared_costs(costs, rank: int, dist, device):
+    """Rank 0's measured costs on every rank (timings differ per GPU; the plan must not)."""
+    import torch
+    t = torch.as_tensor(np.asarray(costs, np.int64), device=device)
+    dist.broadcast(t, src=0)
+    return t.cpu().numpy()
 
 
 def gather_packed(packed, plan: ShardPlan, rank: int, dist, group=None):

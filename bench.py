@@ -2,11 +2,14 @@
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--variant auto|lane|wave]
 
-One step = one frame of the config rendered by all ranks: each rank traces its interleaved
-64x64 shard tiles (atr_make_shard_tiles) into a packed buffer; for N > 1 the packed buffers are
-gathered to rank 0 over RCCL (torch.distributed "nccl") and scattered into the frame there.
-The scene (OBJ load, octree build, upload) is prepared before timing; inputs are resident in
-HBM when the timed region starts. value = traced rays of all ranks / max-over-ranks wall time.
+One step = one frame of the config rendered by all ranks: each rank traces its 64x64 shard tiles
+into a packed buffer; for N > 1 the packed buffers are gathered to rank 0 over RCCL
+(torch.distributed "nccl", async, double-buffered: frame k's gather overlaps frame k+1's render)
+and scattered into the frame there. Tiles are dealt longest-first by cost measured in one
+calibration render on rank 0 (--plan cost, default; --plan rr = round-robin). The scene
+(OBJ load, octree build, upload) and the plan are prepared before timing; inputs are resident
+in HBM when the timed region starts. value = traced rays of all ranks / max-over-ranks wall
+time. ATR_DIST_BACKEND=gloo rehearses N ranks on one GPU (host-staged gather).
 
 Extra JSON fields: roofline (render kernel: algorithmic bytes per launch / average launch time
 from HIP events on the launch stream, against 8 TB/s; traffic = HBM bytes per launch from a
@@ -120,6 +123,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
+                    help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
+    ap.add_argument("--rank0-extra", type=float, default=0.05,
+                    help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
+    ap.add_argument("--check", action="store_true",
+                    help="rank 0: compare the assembled frame with a one-launch full-frame render")
     args = ap.parse_args()
 
     import numpy as np
@@ -127,15 +136,21 @@ def main():
     import torch.distributed as dist
 
     import atray_amd.engine as E
+    from atray_amd import shard as S
     from atray_amd.assets import CENTERS, asset_path
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % ndev)  # ranks > devices only for gloo rehearsals on one GPU
+    dev = torch.device("cuda", local % ndev)
+    backend = os.environ.get("ATR_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     asset, W, H, spp, bounces, use_tree = CONFIGS[args.config]
     variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE,
@@ -144,49 +159,86 @@ def main():
     mesh = E.Mesh.load_obj(asset_path(asset))
     box = mesh.translate_to(mesh.aabb(), CENTERS[asset])
     tree = E.Octree.build(mesh, 300) if use_tree else None
-    eng = E.Engine(local)
+    eng = E.Engine(local % ndev)
     eng.upload([((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)],
                [(mesh, tree, box, 1)])
     cam = E.camera(W, H, spp, bounces)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    all_tiles = [E.make_shard_tiles(W, H, args.side, r, world) for r in range(world)]
-    sizes = [E.packed_size(t) for t in all_tiles]
-    maxn = max(sizes)
-    tiles = E.tiles_array(all_tiles[rank])
-    image = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
-    packed = torch.zeros(maxn, dtype=torch.int32, device=dev)
-    gather = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(world)] if (rank == 0 and world > 1) else None
-    traced = torch.zeros(1, dtype=torch.int64, device=dev)
-    if world == 1:
-        frame = E.atr_frame(E.ATR_LAYOUT_IMAGE, image.data_ptr(), None, None, None, None, None)
+    # shard plan (scene prep, untimed): one calibration render measures every grid tile's cost
+    # on rank 0, broadcast so all ranks derive the same longest-first deal
+    if world > 1 and args.plan == "cost":
+        costs = S.tile_costs(eng, cam, W, H, args.side, SEED) if rank == 0 else np.zeros(
+            len(E.shard_grid(W, H, args.side)), np.int64)
+        costs = S.shared_costs(costs, rank, dist, dev if backend == "nccl" else "cpu")
+        plan = S.ShardPlan.balanced(costs, W, H, world, args.side, args.rank0_extra)
     else:
-        frame = E.atr_frame(E.ATR_LAYOUT_PACKED, packed.data_ptr(), None, None, None, None, None)
-    count_frame = E.atr_frame(frame.layout, frame.framebuffer, None, None, None, None, traced.data_ptr())
-    other_tiles = [E.tiles_array(t) for t in all_tiles]
+        plan = S.ShardPlan(W, H, world, args.side)
+    sizes, maxn = plan.sizes, plan.max_size
+    tiles = E.tiles_array(plan.tiles[rank])
+    image = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
+    # two packed buffers: frame k+1 renders while frame k is gathered
+    packed = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(2)]
+    on_host = world > 1 and backend != "nccl"
+    gather = [[torch.zeros(maxn, dtype=torch.int32, device="cpu" if on_host else dev) for _ in range(world)]
+              for _ in range(2)] if (rank == 0 and world > 1) else None
+    traced = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    def step(fr, evs=None):
+    def frame_of(k):
+        if world == 1:
+            return E.atr_frame(E.ATR_LAYOUT_IMAGE, image.data_ptr(), None, None, None, None, None)
+        return E.atr_frame(E.ATR_LAYOUT_PACKED, packed[k % 2].data_ptr(), None, None, None, None, None)
+
+    frames = [frame_of(0), frame_of(1)]
+    count_frame = E.atr_frame(frames[0].layout, frames[0].framebuffer, None, None, None, None, traced.data_ptr())
+    other_tiles = [E.tiles_array(t) for t in plan.tiles]
+    staging = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(world)] if on_host and rank == 0 else None
+    pending = {}
+
+    def assemble(k):
+        """Rank 0: wait for frame k's gather, scatter every rank's packed pixels into the image."""
+        work = pending.pop(k)
+        if work is not None:
+            work.wait()
+        if rank == 0:
+            for r in range(world):
+                src = gather[k % 2][r]
+                if on_host:
+                    staging[r].copy_(src, non_blocking=False)
+                    src = staging[r]
+                eng.unpack(other_tiles[r], W, src.data_ptr(), image.data_ptr(), stream)
+
+    def step(k, fr, evs=None):
         if evs is not None:
             evs[0].record()
         eng.render_start(cam, tiles, fr, SEED, stream=stream, variant=variant)
         if evs is not None:
             evs[1].record()
         if world > 1:
-            dist.gather(packed, gather if rank == 0 else None, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    eng.unpack(other_tiles[r], W, gather[r].data_ptr(), image.data_ptr(), stream)
+            buf = packed[k % 2]
+            if on_host:
+                torch.cuda.synchronize()
+                buf = buf.cpu()
+            pending[k] = dist.gather(buf, gather[k % 2] if rank == 0 else None, dst=0, async_op=True)
+            if k - 1 in pending:
+                assemble(k - 1)  # the previous frame's scatter, behind this frame's render
+
+    def flush(k):
+        if world > 1 and k in pending:
+            assemble(k)
 
     # rays per frame (all ranks): counted by the kernel (every get_intersection_data call)
-    step(count_frame)
+    step(0, count_frame)
+    flush(0)
     torch.cuda.synchronize()
-    rays_t = traced.clone()
+    rays_t = traced.clone() if backend == "nccl" or world == 1 else traced.cpu()
     if world > 1:
         dist.all_reduce(rays_t)
     rays_per_step = int(rays_t.item())
 
-    for _ in range(args.warmup):
-        step(frame)
+    for k in range(args.warmup):
+        step(k, frames[k % 2])
+    flush(args.warmup - 1)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -194,13 +246,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(frame, evs[k])
+        step(k, frames[k % 2], evs[k])
+    flush(args.steps - 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
@@ -209,6 +262,13 @@ def main():
     # the dominant kernel's work on this rank's tiles, counted by the instrumented build of the
     # same variant (untimed; deterministic)
     live_ctr = eng.counters(cam, tiles, SEED, variant) if rank == 0 else None
+    check = None
+    if args.check and rank == 0:
+        ref = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, ref.data_ptr(), None, None, None, None, None)
+        eng.render_start(cam, [[0, 0, W - 1, H - 1]], fr, SEED, stream=stream)
+        torch.cuda.synchronize()
+        check = int((ref != image).sum().item())
 
     if rank == 0:
         value = rays_per_step * args.steps / elapsed / 1e6
@@ -220,7 +280,11 @@ def main():
                "config": {"workload": f"{args.config}: {asset} {W}x{H} spp={spp} bounces={bounces} "
                                       f"{'octree' if use_tree else 'brute-force'}",
                           "rays_per_step": rays_per_step, "shard_tile": args.side,
-                          "parallelism": f"tiles{world}", "kernel": args.variant}}
+                          "parallelism": f"tiles{world}", "kernel": args.variant,
+                          "plan": args.plan if world > 1 else "single",
+                          "shard_pixels": [int(x) for x in sizes]}}
+        if check is not None:
+            out["check_mismatched_pixels"] = check
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
         clustered = args.variant in ("auto", "cl")

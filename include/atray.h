@@ -110,6 +110,11 @@ int32_t atr_make_tiles(int32_t width, int32_t height, int32_t threads, atr_tile*
    k % world (interleaved for load balance). Returns the count written for `rank`. */
 int32_t atr_make_shard_tiles(int32_t width, int32_t height, int32_t side, int32_t rank,
                              int32_t world, atr_tile* out, int32_t cap);
+/* Cost-balanced alternative: the same side x side grid (row-major, costs[i] per grid tile, e.g.
+   from atr_render_tile_costs) dealt longest-first to the least loaded rank; rank 0 starts with
+   rank0_extra (its frame assembly). Writes owner_out[i] per grid tile; returns the tile count. */
+int32_t atr_balance_shard_tiles(int32_t width, int32_t height, int32_t side, int32_t world,
+                                const int64_t* costs, int64_t rank0_extra, int32_t* owner_out);
 
 /* ---------------------------------------------------------------- device engine */
 typedef struct atr_ctx atr_ctx;
@@ -163,6 +168,11 @@ int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
    counts the full triangle tests it still runs -- and the engine's [4] wave-level triangle
    iterations, [5] DFS passes, [6] all octree box tests, [7] wavefronts, [8] cluster boxes tested
    and [9] primitives screened by the clustered scan. */
+/* Load-balance calibration, synchronous: renders `tiles` once (default kernel) and returns the
+   GPU shader clocks spent per tile (sum over the 8x8 blocks whose area first falls in the tile,
+   list order). Used to deal shard tiles to GPUs by measured cost (atray_amd/shard.py). */
+int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                          uint64_t seed, int64_t* cost_out);
 int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         uint64_t seed, int32_t variant, int64_t counters_out[10]);
 /* Number of pixels a PACKED render of these tiles writes. */

@@ -66,3 +66,81 @@ def test_shard_plan_covers_each_pixel_once(world):
     assert (seen == 1).all()
     assert sum(plan.sizes) == 1920 * 1080
     assert max(plan.sizes) - min(plan.sizes) <= 64 * 64
+
+
+@pytest.mark.parametrize("world", [1, 2, 5, 8])
+def test_balanced_plan_covers_each_pixel_once_and_balances(world):
+    """Cost-balanced deal (atr_balance_shard_tiles): every pixel owned once, deterministic, and
+    the longest-first bound: max load <= mean load + the largest tile cost."""
+    from atray_amd import engine as E
+    from atray_amd.shard import ShardPlan
+    W, H, side = 1920, 1080, 64
+    n = len(E.shard_grid(W, H, side))
+    costs = np.random.default_rng(world).integers(1, 10**6, n) * (np.arange(n) % 7 == 0) + 1
+    plan = ShardPlan.balanced(costs, W, H, world, side)
+    again = ShardPlan.balanced(costs, W, H, world, side)
+    assert np.array_equal(plan.owner, again.owner)
+    seen = np.zeros(W * H, np.int32)
+    for r in range(world):
+        np.add.at(seen, plan.pixel_map(r), 1)
+    assert (seen == 1).all()
+    loads = np.array([costs[plan.owner == r].sum() for r in range(world)])
+    assert loads.max() <= costs.sum() / world + costs.max()
+    extra = ShardPlan.balanced(costs, W, H, world, side, rank0_extra=0.5)
+    if world > 1:
+        l0 = costs[extra.owner == 0].sum()
+        assert l0 <= np.array([costs[extra.owner == r].sum() for r in range(world)]).max()
+
+
+def _bench_worker(rank, world, port, out_path):
+    """The bench's frame-assembly pipeline (double-buffered async gather, lagged scatter) on
+    CPU tensors with the host scatter, fed by oracle hits: the assembled frames must equal the
+    single-process frame for every step."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+
+    from atray_amd import engine as E
+    from atray_amd.assets import CENTERS, asset_path
+    from atray_amd.shard import ShardPlan, scatter_host
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    W, H, side = 160, 96, 32
+    s = O.Scene(asset_path("Monkey"), center=CENTERS["Monkey"])
+    face, _, _ = s.primary_hits(O.Camera(W, H))
+    costs = np.where(np.arange(len(E.shard_grid(W, H, side))) % 3 == 0, 50, 1)
+    plan = ShardPlan.balanced(costs, W, H, world, side, rank0_extra=0.1)
+    m = plan.pixel_map(rank)
+    packed = [torch.zeros(plan.max_size, dtype=torch.int64) for _ in range(2)]
+    gather = [[torch.zeros(plan.max_size, dtype=torch.int64) for _ in range(world)] for _ in range(2)]
+    pending, frames = {}, []
+    for k in range(5):
+        packed[k % 2].zero_()
+        packed[k % 2][:len(m)] = torch.from_numpy(face.ravel()[m].astype(np.int64) + k)
+        pending[k] = dist.gather(packed[k % 2], gather[k % 2] if rank == 0 else None, dst=0, async_op=True)
+        if k - 1 in pending:
+            pending.pop(k - 1).wait()
+            if rank == 0:
+                frames.append(scatter_host([t.numpy() for t in gather[(k - 1) % 2]], plan))
+    pending.pop(4).wait()
+    if rank == 0:
+        frames.append(scatter_host([t.numpy() for t in gather[0]], plan))
+        np.save(out_path, np.stack(frames))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_pipelined_gather_reassembles_every_frame(tmp_path):
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_bench_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    frames = np.load(out)
+    from atray_amd.assets import CENTERS, asset_path
+    from oracle import oracle as O
+    s = O.Scene(asset_path("Monkey"), center=CENTERS["Monkey"])
+    face, _, _ = s.primary_hits(O.Camera(160, 96))
+    assert len(frames) == 5
+    for k in range(5):
+        assert np.array_equal(frames[k], face.astype(np.int64) + k)
