@@ -840,18 +840,25 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     if (nb) HIPCHK(hipMemcpy(h.data(), cost, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     HIPCHK(hipFree(fb));
     HIPCHK(hipFree(cost));
-    // a block belongs to the first tile (list order) that holds its origin pixel
+    // a block (one 8x8 cell of the image grid) belongs to the first tile (list order) that
+    // overlaps it: paint cell owners in list order, first writer wins
+    const int32_t cw = (cam->width + 7) / 8, chh = (cam->height + 7) / 8;
+    std::vector<int32_t> owner(size_t(cw) * size_t(chh), -1);
+    for (int32_t t = 0; t < ntiles; ++t) {
+        const atr_tile& T = tiles[t];
+        const int32_t x0 = std::max(0, T.min_x) / 8, x1 = std::min(cam->width - 1, T.max_x) / 8;
+        const int32_t y0 = std::max(0, T.min_y) / 8, y1 = std::min(cam->height - 1, T.max_y) / 8;
+        for (int32_t cy = y0; cy <= y1; ++cy)
+            for (int32_t cx = x0; cx <= x1; ++cx) {
+                int32_t& o = owner[size_t(cy) * size_t(cw) + size_t(cx)];
+                if (o < 0) o = t;
+            }
+    }
     for (int32_t t = 0; t < ntiles; ++t) cost_out[t] = 0;
     for (size_t k = 0; k < nb; ++k) {
         const DBlock& b = bs->host[k];
-        for (int32_t t = 0; t < ntiles; ++t) {
-            const atr_tile& T = tiles[t];
-            const int32_t x = std::max(b.x0, T.min_x), y = std::max(b.y0, T.min_y);
-            if (x <= T.max_x && y <= T.max_y && x < b.x0 + 8 && y < b.y0 + 8) {
-                cost_out[t] += int64_t(h[k]);
-                break;
-            }
-        }
+        const int32_t o = owner[size_t(b.y0 / 8) * size_t(cw) + size_t(b.x0 / 8)];
+        if (o >= 0) cost_out[o] += int64_t(h[k]);
     }
     return ATR_OK;
 }

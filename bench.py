@@ -123,6 +123,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="frames in flight (one HIP stream each); 1 = strictly one frame at a time")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
@@ -176,60 +178,65 @@ def main():
         plan = S.ShardPlan(W, H, world, args.side)
     sizes, maxn = plan.sizes, plan.max_size
     tiles = E.tiles_array(plan.tiles[rank])
-    image = torch.zeros(W * H, dtype=torch.int32, device=dev) if rank == 0 else None
-    # two packed buffers: frame k+1 renders while frame k is gathered
-    packed = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(2)]
+    # S frames in flight, one HIP stream and one set of output buffers each: frame k renders on
+    # stream k % S while earlier frames finish, are gathered (N > 1) and assembled on rank 0
+    S_ = max(1, args.streams)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S_ - 1)]
+    images = [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(S_)] if rank == 0 else None
+    packed = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(S_)] if world > 1 else None
     on_host = world > 1 and backend != "nccl"
     gather = [[torch.zeros(maxn, dtype=torch.int32, device="cpu" if on_host else dev) for _ in range(world)]
-              for _ in range(2)] if (rank == 0 and world > 1) else None
+              for _ in range(S_)] if (rank == 0 and world > 1) else None
     traced = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    def frame_of(k):
+    def frame_of(slot, count=False):
         if world == 1:
-            return E.atr_frame(E.ATR_LAYOUT_IMAGE, image.data_ptr(), None, None, None, None, None)
-        return E.atr_frame(E.ATR_LAYOUT_PACKED, packed[k % 2].data_ptr(), None, None, None, None, None)
+            fb, layout = images[slot], E.ATR_LAYOUT_IMAGE
+        else:
+            fb, layout = packed[slot], E.ATR_LAYOUT_PACKED
+        return E.atr_frame(layout, fb.data_ptr(), None, None, None, None, traced.data_ptr() if count else None)
 
-    frames = [frame_of(0), frame_of(1)]
-    count_frame = E.atr_frame(frames[0].layout, frames[0].framebuffer, None, None, None, None, traced.data_ptr())
+    frames = [frame_of(q) for q in range(S_)]
     other_tiles = [E.tiles_array(t) for t in plan.tiles]
     staging = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(world)] if on_host and rank == 0 else None
     pending = {}
 
     def assemble(k):
-        """Rank 0: wait for frame k's gather, scatter every rank's packed pixels into the image."""
+        """Frame k's gather done (its stream waits on it); rank 0 scatters every rank's packed
+        pixels into that slot's image, on the frame's stream."""
+        q = k % S_
         work = pending.pop(k)
-        if work is not None:
-            work.wait()
-        if rank == 0:
-            for r in range(world):
-                src = gather[k % 2][r]
-                if on_host:
-                    staging[r].copy_(src, non_blocking=False)
-                    src = staging[r]
-                eng.unpack(other_tiles[r], W, src.data_ptr(), image.data_ptr(), stream)
+        with torch.cuda.stream(streams[q]):
+            if work is not None:
+                work.wait()
+            if rank == 0:
+                for r in range(world):
+                    src = gather[q][r]
+                    if on_host:
+                        staging[r].copy_(src, non_blocking=False)
+                        src = staging[r]
+                    eng.unpack(other_tiles[r], W, src.data_ptr(), images[q].data_ptr(), streams[q].cuda_stream)
 
-    def step(k, fr, evs=None):
-        if evs is not None:
-            evs[0].record()
-        eng.render_start(cam, tiles, fr, SEED, stream=stream, variant=variant)
-        if evs is not None:
-            evs[1].record()
+    def step(k, fr):
+        q = k % S_
+        eng.render_start(cam, tiles, fr, SEED, stream=streams[q].cuda_stream, variant=variant)
         if world > 1:
-            buf = packed[k % 2]
-            if on_host:
-                torch.cuda.synchronize()
-                buf = buf.cpu()
-            pending[k] = dist.gather(buf, gather[k % 2] if rank == 0 else None, dst=0, async_op=True)
-            if k - 1 in pending:
-                assemble(k - 1)  # the previous frame's scatter, behind this frame's render
+            with torch.cuda.stream(streams[q]):
+                buf = packed[q]
+                if on_host:
+                    torch.cuda.synchronize()
+                    buf = buf.cpu()
+                pending[k] = dist.gather(buf, gather[q] if rank == 0 else None, dst=0, async_op=True)
+            if k - S_ + 1 in pending:
+                assemble(k - S_ + 1)  # the oldest frame in flight, before its slot is reused
 
-    def flush(k):
-        if world > 1 and k in pending:
+    def flush():
+        for k in sorted(pending):
             assemble(k)
 
     # rays per frame (all ranks): counted by the kernel (every get_intersection_data call)
-    step(0, count_frame)
-    flush(0)
+    step(0, frame_of(0, count=True))
+    flush()
     torch.cuda.synchronize()
     rays_t = traced.clone() if backend == "nccl" or world == 1 else traced.cpu()
     if world > 1:
@@ -237,17 +244,16 @@ def main():
     rays_per_step = int(rays_t.item())
 
     for k in range(args.warmup):
-        step(k, frames[k % 2])
-    flush(args.warmup - 1)
+        step(k, frames[k % S_])
+    flush()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k, frames[k % 2], evs[k])
-    flush(args.steps - 1)
+        step(k, frames[k % S_])
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -256,6 +262,14 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # roofline: the render kernel's own average duration, launches serialized on one stream
+    # (HIP events on that stream; rocprofv3 of `bench.py --streams 1` reports the same kernel)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for a, b in evs:
+        a.record(streams[0])
+        eng.render_start(cam, tiles, frames[0], SEED, stream=streams[0].cuda_stream, variant=variant)
+        b.record(streams[0])
+    torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     rc, _ = eng.wait()
     assert rc == 0
@@ -268,7 +282,7 @@ def main():
         fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, ref.data_ptr(), None, None, None, None, None)
         eng.render_start(cam, [[0, 0, W - 1, H - 1]], fr, SEED, stream=stream)
         torch.cuda.synchronize()
-        check = int((ref != image).sum().item())
+        check = sum(int((ref != im).sum().item()) for im in images)
 
     if rank == 0:
         value = rays_per_step * args.steps / elapsed / 1e6
@@ -281,7 +295,7 @@ def main():
                                       f"{'octree' if use_tree else 'brute-force'}",
                           "rays_per_step": rays_per_step, "shard_tile": args.side,
                           "parallelism": f"tiles{world}", "kernel": args.variant,
-                          "plan": args.plan if world > 1 else "single",
+                          "plan": args.plan if world > 1 else "single", "frames_in_flight": args.streams,
                           "shard_pixels": [int(x) for x in sizes]}}
         if check is not None:
             out["check_mismatched_pixels"] = check

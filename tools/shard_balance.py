@@ -22,15 +22,25 @@ from atray_amd import shard as S  # noqa: E402
 from bench import CONFIGS, SEED  # noqa: E402
 
 
+STREAMS = [None]
+
+
 def timed(eng, cam, tiles, fr, stream, iters):
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    """ms per frame with len(STREAMS) frames in flight (one stream each), as bench.py runs."""
     eng.render_start(cam, tiles, fr, SEED, stream=stream)
-    a.record()
-    for _ in range(iters):
-        eng.render_start(cam, tiles, fr, SEED, stream=stream)
-    b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / iters
+    t0 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for k in range(iters * len(STREAMS)):
+        s = STREAMS[k % len(STREAMS)]
+        eng.render_start(cam, tiles, fr, SEED, stream=s.cuda_stream)
+    ends = []
+    for s in STREAMS:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(s)
+        ends.append(e)
+    torch.cuda.synchronize()
+    return max(t0.elapsed_time(e) for e in ends) / (iters * len(STREAMS))
 
 
 def main():
@@ -40,7 +50,9 @@ def main():
     ap.add_argument("--sides", default="32,64")
     ap.add_argument("--plans", default="rr,lpt")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--streams", type=int, default=1)
     args = ap.parse_args()
+    STREAMS[:] = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     asset, W, H, spp, bounces, use_tree = CONFIGS[args.config]
     mesh = E.Mesh.load_obj(asset_path(asset))
     box = mesh.translate_to(mesh.aabb(), CENTERS[asset])
@@ -53,7 +65,7 @@ def main():
     packed = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     fr = E.atr_frame(E.ATR_LAYOUT_PACKED, packed.data_ptr(), None, None, None, None, None)
     full = timed(eng, cam, [[0, 0, W - 1, H - 1]], fr, stream, args.iters)
-    out = {"config": args.config, "full_frame_ms": round(full, 4), "runs": []}
+    out = {"config": args.config, "streams": args.streams, "full_frame_ms": round(full, 4), "runs": []}
     for plan in args.plans.split(","):
         for side in [int(x) for x in args.sides.split(",")]:
             for world in [int(x) for x in args.worlds.split(",")]:
