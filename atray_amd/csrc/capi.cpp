@@ -99,6 +99,11 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     }
 }
 
+int32_t xcd_chunk() {  // EXPERIMENT knob (ATR_XCD_CHUNK), read once
+    static const int32_t v = [] { const char* e = std::getenv("ATR_XCD_CHUNK"); return e ? std::atoi(e) : 0; }();
+    return v;
+}
+
 }  // namespace
 
 struct atr_ctx {
@@ -111,7 +116,7 @@ struct atr_ctx {
     std::vector<DevBuf> scene_bufs;
     DScene* d_scene = nullptr;
     int64_t scene_bytes = 0;
-    int32_t max_nodes = 0, max_depth = 0, nmodels = 0;
+    int32_t max_nodes = 0, max_depth = 0, nmodels = 0, max_inner = 0;
     int cluster_size = 16;     // primitives per leaf cluster (ATR_CLUSTER_SIZE overrides, 1..32)
     int64_t nclusters = 0;
     static constexpr int kBlockSlots = 24;  // tile-list cache: own render + one unpack per rank
@@ -495,6 +500,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
     S.nmodels = nmodels;
     c->max_nodes = 0;
     c->max_depth = 0;
+    c->max_inner = 0;
     c->nclusters = 0;
     if (const char* e = std::getenv("ATR_CLUSTER_SIZE")) {
         const int v = std::atoi(e);
@@ -614,6 +620,15 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
             }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
             dm.nodes = static_cast<const DNode*>(p);
+            {
+                std::vector<float4_t> inner;
+                if ((rc = inner_table(T, inner))) return rc;
+                dm.ninner = int32_t(inner.size() / 3);
+                if (inner.empty()) inner.assign(3, float4_t{0.f, 0.f, 0.f, 0.f});
+                if ((rc = dev_upload(c, inner.data(), inner.size() * sizeof(float4_t), &p))) return rc;
+                dm.inner = static_cast<const float4_t*>(p);
+                if (dm.ninner > c->max_inner) c->max_inner = dm.ninner;
+            }
             if ((rc = dev_upload(c, range.data(), range.size() * sizeof(uint32_t), &p))) return rc;
             dm.leaf_range = static_cast<const uint32_t*>(p);
             if ((rc = dev_upload(c, tris.data(), tris.size() * sizeof(DTri), &p))) return rc;
@@ -764,6 +779,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     P.counters = nullptr;
+    P.xcd_chunk = xcd_chunk();
     const int wave = sched_of(variant);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(atr_launch_render(P, wave, s));
@@ -772,6 +788,41 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     c->have_render = true;
     c->last_stream = s;
     c->last_ntiles = ntiles;
+    return ATR_OK;
+}
+
+int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                          uint64_t seed, int32_t variant, uint64_t* out, int64_t cap, int64_t* nblocks) {
+    if (!c || !cam || !nblocks || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
+    if (!bs) return rc;
+    const size_t nb = bs->host.size();
+    *nblocks = int64_t(nb);
+    if (!out || cap < int64_t(3 * nb)) return ATR_OK;  // size query
+    void* fb = nullptr;
+    void* tr = nullptr;
+    HIPCHK(hipMalloc(&fb, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
+    HIPCHK(hipMalloc(&tr, std::max<size_t>(1, 3 * nb) * sizeof(unsigned long long)));
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.blocks = static_cast<const DBlock*>(bs->dev.p);
+    P.nblocks = int32_t(nb);
+    P.layout = ATR_LAYOUT_PACKED;
+    P.framebuffer = static_cast<uint32_t*>(fb);
+    P.error_flag = c->d_error;
+    P.wave_trace = static_cast<unsigned long long*>(tr);
+    P.xcd_chunk = xcd_chunk();
+    HIPCHK(atr_launch_render(P, sched_of(variant), nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    if (nb) HIPCHK(hipMemcpy(out, tr, 3 * nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(fb));
+    HIPCHK(hipFree(tr));
     return ATR_OK;
 }
 

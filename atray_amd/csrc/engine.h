@@ -90,6 +90,11 @@ static_assert(sizeof(DTri) == 48, "DTri layout");
 // Per-model device view. has_tree == 0 selects the brute-force branch (renderer.cpp:58-82).
 struct DModel {
     const DNode* nodes;          // octree nodes in reference order (root = 0)
+    // inner nodes only: 3 float4 = {lo.xyz, v.x}{v.yz, hi.xy}{hi.z, bits(first
+    // child node), bits(parent inner id), bits((inner id of first inner child << 8) | leaf mask)};
+    // the children boxes are derived from lo, v, hi (kd_tree.cpp:116-148)
+    const float4_t* inner;
+    int32_t ninner;
     const uint32_t* leaf_range;  // 2 u32 per node: first DTri, count (leaves only)
     const DTri* tris;            // leaf-ordered primitives (tree) or face-ordered (brute force)
     // the same primitives as SoA streams for per-lane loads: t0 = {a.xyz, ab.x},
@@ -158,6 +163,8 @@ struct RenderParams {
     int32_t* error_flag;  // set to 1 if a ray hit a traversal limit (never for depth <= 16)
     unsigned long long* counters;  // non-null -> instrumented kernel (10 u64, see render.hip)
     unsigned long long* block_cost;  // non-null -> shader clocks spent per block (load balance)
+    unsigned long long* wave_trace;  // non-null -> per block: start, end (100 MHz clock), HW_ID | XCC_ID << 32
+    int32_t xcd_chunk;  // 0: contiguous block range per XCD; k > 0: k-workgroup chunks dealt round-robin
 };
 
 }  // namespace atr

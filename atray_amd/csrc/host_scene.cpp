@@ -361,6 +361,49 @@ int atr::leaf_clusters(const HostTree& T, int size, LeafClusters& C) {
     return ATR_OK;
 }
 
+int atr::inner_table(const HostTree& T, std::vector<float4_t>& out) {
+    const int32_t n = T.nnodes;
+    std::vector<int32_t> rank(size_t(n), -1);
+    int32_t ninner = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (T.children[size_t(i)]) rank[size_t(i)] = ninner++;
+    out.assign(3 * size_t(ninner), float4_t{0.f, 0.f, 0.f, 0.f});
+    auto same = [](float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; };
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t c = T.children[size_t(i)];
+        if (!c) continue;
+        if (c < 0 || c + 8 > n) return ATR_E_INVALID;
+        const float* b = &T.bounds[6 * size_t(i)];
+        const float* b0 = &T.bounds[6 * size_t(c)];
+        const float lo[3] = {b[0], b[1], b[2]}, hi[3] = {b[3], b[4], b[5]};
+        const float v[3] = {b0[3], b0[4], b0[5]};  // bb_left.aabb.max = division point
+        uint32_t leafm = 0;
+        int32_t base = -1;
+        for (int k = 0; k < 8; ++k) {
+            const float* cb = &T.bounds[6 * size_t(c + k)];
+            const int bit[3] = {k >> 2, (k >> 1) & 1, k & 1};  // x: left/right, y: bottom/top, z: back/front
+            for (int a = 0; a < 3; ++a) {
+                const float mn = bit[a] ? v[a] : lo[a], mx = bit[a] ? hi[a] : v[a];
+                if (!same(cb[a], mn) || !same(cb[3 + a], mx)) return ATR_E_TREE_LAYOUT;
+            }
+            if (T.children[size_t(c + k)] == 0) leafm |= 1u << k;
+            else if (base < 0) base = rank[size_t(c + k)];
+        }
+        if (base < 0) base = 0;
+        const int32_t par = T.parent.empty() || T.parent[size_t(i)] < 0 ? -1 : rank[size_t(T.parent[size_t(i)])];
+        const uint32_t bm = (uint32_t(base) << 8) | leafm;
+        float w[3];
+        std::memcpy(&w[0], &c, 4);
+        std::memcpy(&w[1], &par, 4);
+        std::memcpy(&w[2], &bm, 4);
+        float4_t* r = &out[3 * size_t(rank[size_t(i)])];
+        r[0] = float4_t{lo[0], lo[1], lo[2], v[0]};
+        r[1] = float4_t{v[1], v[2], hi[0], hi[1]};
+        r[2] = float4_t{hi[2], w[0], w[1], w[2]};
+    }
+    return ATR_OK;
+}
+
 int atr::octree_finish(HostTree& T) {  // parents/depths for a caller-provided tree
     const int32_t n = T.nnodes;
     T.parent.assign(size_t(n), -1);

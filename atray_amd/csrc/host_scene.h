@@ -40,6 +40,12 @@ struct LeafClusters {
 };
 int leaf_clusters(const HostTree& T, int size, LeafClusters& C);
 
+// Inner-node table for the derived-box traversal: 3 float4 per inner node, in
+// reference node order (inner id = rank among inner nodes). Fails with ATR_E_TREE_LAYOUT unless
+// every inner node's 8 children boxes are the (lo|v, v|hi) combinations of its box and split
+// point, bit for bit, as build_oct_kd_tree makes them (kd_tree.cpp:116-148).
+int inner_table(const HostTree& T, std::vector<float4_t>& out);
+
 int parse_obj_text(const char* text, size_t len, HostMesh& m);
 void mesh_aabb(const HostMesh& m, float out[6]);
 void mesh_translate(HostMesh& m, float box[6], V3 c);

@@ -157,6 +157,9 @@ __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m
         tn = fmaxf(fmaxf(nx - gt * ax, ny - gt * ay), nz - gt * az);
         tf = fminf(fminf(fx1 + gt * ax, fy1 + gt * ay), fz1 + gt * az);
         const bool tight = !(tn > tf || tf < 0.f || tn > best_t);
+#ifdef ATR_EXP_SKIP_LOOSE
+        if (!tight) continue;  // EXPERIMENT ONLY (not exact): cost of the loose-only screens
+#endif
         const float mg = 16.0f * kEps * P;
         const float dlo = kTol - mg, dhi = tight ? __builtin_inff() : kTau + mg;
         const uint32_t first = __float_as_uint(hi.w);
@@ -216,7 +219,7 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
         bool more = true;
         while (more) {
             LeafBuf<K> lb;
-            const int32_t n = traverse_pass<K, COUNT>(r, m.nodes, lb, bd, bi, ct);
+            const int32_t n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
             if (n < 0) { err = 1; break; }
             int32_t nb = n < K ? n : K;
             more = n > K;
@@ -251,7 +254,7 @@ __device__ __forceinline__ int32_t tq_next_leaf(TreeQuery& q, const Ray& r, cons
     for (;;) {
         if (q.state == 2) return -1;
         if (q.state == 0) {
-            q.ncand = traverse_pass<kLeafBuf, COUNT>(r, m.nodes, q.lb, q.bd, q.bi, ct);
+            q.ncand = traverse_pass<kLeafBuf, COUNT>(r, m.inner, q.lb, q.bd, q.bi, ct);
             if (q.ncand < 0) { err = 1; q.state = 2; return -1; }
             q.pos = 0;
             q.state = 1;
@@ -356,7 +359,7 @@ __device__ __forceinline__ int32_t tile_next_leaf(TreeQuery& q, const Ray& r, co
     for (;;) {
         if (q.state == 2) return -1;
         if (q.state == 0) {
-            q.ncand = traverse_pass<kLeafBuf, COUNT>(r, m.nodes, q.lb, q.bd, q.bi, ct);
+            q.ncand = traverse_pass<kLeafBuf, COUNT>(r, m.inner, q.lb, q.bd, q.bi, ct);
             if (q.ncand < 0) { err = 1; q.state = 2; return -1; }
             q.pos = q.ncand < kLeafBuf ? q.ncand : kLeafBuf;  // entries left in the buffer
             q.state = 1;
@@ -625,9 +628,18 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
     return ret;
 }
 
-__device__ __forceinline__ int remap_xcd(int wg, int nwg) {
+__device__ __forceinline__ int remap_xcd(int wg, int nwg, int chunk) {
+    const int x = wg % 8;  // the hardware deals workgroups round-robin over the 8 XCDs
+    if (chunk > 0) {
+        // chunks of `chunk` consecutive workgroups dealt round-robin to the XCDs: neighbouring
+        // cells still share an XCD (and its L2), every XCD gets chunks from the whole frame
+        const int span = 8 * chunk, full = (nwg / span) * span;
+        if (wg >= full) return wg;
+        const int j = wg / 8;
+        return ((j / chunk) * 8 + x) * chunk + j % chunk;
+    }
     // consecutive work blocks -> same XCD (its L2 holds their shared leaves); bijective form
-    const int q = nwg / 8, rm = nwg % 8, x = wg % 8;
+    const int q = nwg / 8, rm = nwg % 8;
     return (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + wg / 8;
 }
 
@@ -640,7 +652,7 @@ template <int SCHED, bool COUNT, bool PRIMARY, int OCC = 4>
 __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(RenderParams P) {
     constexpr int NW = sched_waves(SCHED);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = remap_xcd(blockIdx.x, gridDim.x) * NW + wave;
+    const int b = remap_xcd(blockIdx.x, gridDim.x, P.xcd_chunk) * NW + wave;
     if (SCHED != SCHED_TILE4 && SCHED != SCHED_TILE8 && b >= P.nblocks) return;  // whole wavefront
     const bool in_range = b < P.nblocks;
     DBlock blk;
@@ -650,6 +662,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     const bool active = (mask >> lane) & 1;
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
     const uint64_t clk0 = P.block_cost ? clock64() : 0;
+    const uint64_t rt0 = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const atr_camera& cm = P.cam;
     const DScene* S = P.scene;
     int err = 0;
@@ -714,6 +727,14 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     }
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
     if (P.block_cost && lane == 0 && in_range) P.block_cost[b] = clock64() - clk0;
+    if (P.wave_trace && lane == 0 && in_range) {  // diagnostic: where and when this wave ran
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        P.wave_trace[3 * size_t(b)] = rt0;
+        P.wave_trace[3 * size_t(b) + 1] = __builtin_amdgcn_s_memrealtime();
+        P.wave_trace[3 * size_t(b) + 2] = uint64_t(hw) | (uint64_t(xcc) << 32);
+    }
     if constexpr (COUNT) {
         // counters[0..9]: rays, box(ref), tri, leaf, wave_tri_iters, passes, box_all, waves,
         // cluster boxes, screened primitives

@@ -185,31 +185,73 @@ __device__ __forceinline__ int32_t lb_node(const LeafBuf<K>& b, int j) {
     return r;
 }
 
+// One inner node of the derived-box table (engine.h DModel::inner).
+struct Inner {
+    float lx, ly, lz, vx, vy, vz, hx, hy, hz;
+    int32_t child;   // children_start_position (node index of child 0)
+    int32_t parent;  // parent's inner id, -1 at the root
+    uint32_t bm;     // (inner id of the first inner child << 8) | leaf-children mask
+};
+
+__device__ __forceinline__ Inner load_inner(const float4_t* __restrict__ tab, int32_t i) {
+    const float4_t a = tab[3 * i], b = tab[3 * i + 1], c = tab[3 * i + 2];
+    Inner n;
+    n.lx = a.x; n.ly = a.y; n.lz = a.z; n.vx = a.w;
+    n.vy = b.x; n.vz = b.y; n.hx = b.z; n.hy = b.w;
+    n.hz = c.x;
+    n.child = __float_as_int(c.y);
+    n.parent = __float_as_int(c.z);
+    n.bm = __float_as_uint(c.w);
+    return n;
+}
+
 // Examine the children of an inner node (kd_tree.cpp:370-434): box-test children in order
 // until 5 have been hit; inner hits -> returned bit mask, leaf hits -> leaf order buffer.
+// The children boxes are the octants of (lo, v, hi) (kd_tree.cpp:116-148), so every slab
+// value a child test needs is one of three per axis, (b - o) * inv for b in {lo, v, hi}: the
+// same f32 operations on the same operands as the reference's per-child slab test
+// (aabb.h:29-93), hence the same bits, computed once per node instead of per child and with
+// no child box loads. Child k: x half = k >> 2, y half = (k >> 1) & 1, z half = k & 1.
 template <int K, bool COUNT>
-__device__ __forceinline__ uint32_t examine_children(const Ray& r, const DNode* __restrict__ nodes,
-                                                     int32_t first, LeafBuf<K>& lb, int32_t& disc,
-                                                     int32_t& ncand, float bd, int32_t bi, Ctr& ct,
-                                                     bool first_pass) {
+__device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, LeafBuf<K>& lb, int32_t& disc,
+                                                  int32_t& ncand, float bd, int32_t bi, Ctr& ct,
+                                                  bool first_pass) {
+    const float X0 = (n.lx - r.o.x) * r.inv.x, X1 = (n.vx - r.o.x) * r.inv.x, X2 = (n.hx - r.o.x) * r.inv.x;
+    const float Y0 = (n.ly - r.o.y) * r.inv.y, Y1 = (n.vy - r.o.y) * r.inv.y, Y2 = (n.hy - r.o.y) * r.inv.y;
+    const float Z0 = (n.lz - r.o.z) * r.inv.z, Z1 = (n.vz - r.o.z) * r.inv.z, Z2 = (n.hz - r.o.z) * r.inv.z;
+    // near/far slab value of the low (0) and high (1) half per axis: bounds[inv_signs] is the
+    // max when the inverse direction is negative (aabb.h:33-34)
+    const float nx0 = r.s0 ? X1 : X0, nx1 = r.s0 ? X2 : X1, fx0 = r.s0 ? X0 : X1, fx1 = r.s0 ? X1 : X2;
+    const float ny0 = r.s1 ? Y1 : Y0, ny1 = r.s1 ? Y2 : Y1, fy0 = r.s1 ? Y0 : Y1, fy1 = r.s1 ? Y1 : Y2;
+    const float nz0 = r.s2 ? Z1 : Z0, nz1 = r.s2 ? Z2 : Z1, fz0 = r.s2 ? Z0 : Z1, fz1 = r.s2 ? Z1 : Z2;
     uint32_t mask = 0;
     int nodes_hit = 0;
-    for (int i = 0; i < 8 && nodes_hit <= 4; ++i) {
-        const NodeBox c = load_node(nodes, first + i);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (nodes_hit > 4) break;
         if constexpr (COUNT) { ct.box_all += 1; ct.box += first_pass ? 1u : 0u; }
-        if (c.children != 0) {
-            if (box_check(r, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz)) {
+        float tmin = (i >> 2) ? nx1 : nx0, tmax = (i >> 2) ? fx1 : fx0;
+        const float tymin = ((i >> 1) & 1) ? ny1 : ny0, tymax = ((i >> 1) & 1) ? fy1 : fy0;
+        const float tzmin = (i & 1) ? nz1 : nz0, tzmax = (i & 1) ? fz1 : fz0;
+        bool in = !((tmin > tymax) || (tymin > tmax));
+        if (tymin > tmin) tmin = tymin;
+        if (tymax < tmax) tmax = tymax;
+        in = in && !((tmin > tzmax) || (tzmin > tmax));
+        if (!((n.bm >> i) & 1u)) {  // inner child: check_ray_AABB_intersection (aabb.h:65-93)
+            if (in) {
                 ++nodes_hit;
                 mask |= 1u << i;
             }
-        } else {
-            const float dis = box_entry(r, c.lx, c.ly, c.lz, c.hx, c.hy, c.hz);
+        } else {  // leaf child: get_ray_AABB_intersection (aabb.h:29-63)
+            if (tzmin > tmin) tmin = tzmin;
+            if (tzmax < tmax) tmax = tzmax;
+            const float dis = !in ? 0.0f : (tmin > 0 ? tmin : (tmax > 0 ? tmax : 0.0f));
             if (dis > 0.0f) {
                 ++nodes_hit;
                 const int32_t id = disc++;
                 if (dis > bd || (dis == bd && id > bi)) {
                     ++ncand;
-                    lb_insert<K>(lb, dis, first + i, id);
+                    lb_insert<K>(lb, dis, n.child + i, id);
                 }
             }
         }
@@ -220,37 +262,43 @@ __device__ __forceinline__ uint32_t examine_children(const Ray& r, const DNode* 
 // One DFS pass over the inner nodes (the reference's hit-stack loop, kd_tree.cpp:363-435),
 // keeping the K first leaves (in sorted order) strictly after (bd, bi). Returns the number of
 // candidate leaves after the bound, or -1 if the tree is deeper than the mask stack.
+// Per level the stack keeps only the 8-bit mask of inner children still to visit (popped
+// highest first = the reference's LIFO order); a descent reads the child's 48-B record, an
+// ascent the last 16 B of the parent's.
 template <int K, bool COUNT>
-__device__ __forceinline__ int32_t traverse_pass(const Ray& r, const DNode* __restrict__ nodes,
+__device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* __restrict__ tab,
                                                  LeafBuf<K>& lb, float bd, int32_t bi, Ctr& ct) {
     const bool first_pass = bi < 0;
     if constexpr (COUNT) ct.pass += 1;
     lb_clear<K>(lb);
     int32_t disc = 0, ncand = 0;
-    const NodeBox root = load_node(nodes, 0);
-    uint64_t lo = examine_children<K, COUNT>(r, nodes, root.children, lb, disc, ncand, bd, bi, ct, first_pass);
+    Inner cur = load_inner(tab, 0);
+    uint64_t lo = examine_inner<K, COUNT>(r, cur, lb, disc, ncand, bd, bi, ct, first_pass);
     uint64_t hi = 0;
-    int32_t p = 0, pfirst = root.children, lvl = 0;
+    uint32_t bm = cur.bm;
+    int32_t parent = -1, lvl = 0;
     for (;;) {
         const uint32_t m = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
         if (m) {
             const int s = 31 - __clz(m);
             if (lvl < 8) lo &= ~(uint64_t(1) << (8 * lvl + s));
             else hi &= ~(uint64_t(1) << (8 * (lvl - 8) + s));
-            const int32_t c = pfirst + s;
-            const NodeBox cn = load_node(nodes, c);
-            const uint64_t cm = examine_children<K, COUNT>(r, nodes, cn.children, lb, disc, ncand, bd, bi, ct, first_pass);
+            const uint32_t innerm = ~bm & ((1u << s) - 1u);  // inner children before s
+            const int32_t id = int32_t(bm >> 8) + __popc(innerm);
+            cur = load_inner(tab, id);
+            const uint64_t cm = examine_inner<K, COUNT>(r, cur, lb, disc, ncand, bd, bi, ct, first_pass);
             ++lvl;
             if (lvl >= kMaskLevels) return -1;
             if (lvl < 8) lo |= cm << (8 * lvl);
             else hi |= cm << (8 * (lvl - 8));
-            p = c;
-            pfirst = cn.children;
+            bm = cur.bm;
+            parent = cur.parent;
         } else {
             if (lvl == 0) break;
             --lvl;
-            p = load_node(nodes, p).parent;
-            pfirst = load_node(nodes, p).children;
+            const float4_t t = tab[3 * parent + 2];
+            bm = __float_as_uint(t.w);
+            parent = __float_as_int(t.z);
         }
     }
     return ncand;

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_traverse(WFParams W, int32_t mode
                 } else {
                     LeafBuf<kLeafBuf> lb;
                     Ctr ct;
-                    const int32_t nc = traverse_pass<kLeafBuf, false>(ray, m.nodes, lb, -kInf, -1, ct);
+                    const int32_t nc = traverse_pass<kLeafBuf, false>(ray, m.inner, lb, -kInf, -1, ct);
                     if (nc < 0) { atomicOr(W.error_flag, 1); }
                     else leaf = wf_store_pass(W, r, lb, nc);
                 }
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_rewalk(WFParams W, int32_t model,
             const Ray ray = wf_ray(W, r);
             LeafBuf<kLeafBuf> lb;
             Ctr ct;
-            const int32_t nc = traverse_pass<kLeafBuf, false>(ray, m.nodes, lb, W.qd7[r], W.qi7[r], ct);
+            const int32_t nc = traverse_pass<kLeafBuf, false>(ray, m.inner, lb, W.qd7[r], W.qi7[r], ct);
             if (nc < 0) atomicOr(W.error_flag, 1);
             else leaf = wf_store_pass(W, r, lb, nc);
         }

@@ -15,7 +15,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libatray_hip.so")
+LIB_PATH = os.environ.get("ATRAY_LIB") or os.path.join(HERE, "_lib", "libatray_hip.so")  # ATRAY_LIB: experiment builds only
 
 ATR_LAYOUT_IMAGE = 0
 ATR_LAYOUT_PACKED = 1
@@ -26,7 +26,7 @@ MISS = 0xFFFFFFFF
 MAX_FLOAT = np.float32(3.402823466e38)
 
 ERRORS = {-1: "ATR_E_INVALID", -2: "ATR_E_IO", -3: "ATR_E_NOMEM", -4: "ATR_E_NOSCENE",
-          -5: "ATR_E_TREE_DEPTH"}
+          -5: "ATR_E_TREE_DEPTH", -6: "ATR_E_TREE_LAYOUT"}
 
 
 class AtrError(RuntimeError):
@@ -88,7 +88,7 @@ EXPORTS = [
     "atr_octree_from_nodes", "atr_octree_free", "atr_octree_export", "atr_octree_stats", "atr_camera_set",
     "atr_make_tiles", "atr_make_shard_tiles", "atr_create", "atr_destroy", "atr_version",
     "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
-    "atr_render_counters", "atr_render_tile_costs", "atr_balance_shard_tiles",
+    "atr_render_counters", "atr_render_tile_costs", "atr_render_wave_trace", "atr_balance_shard_tiles",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d",
@@ -135,6 +135,7 @@ def lib():
         "atr_render_packed_size": ([vp, i32], i64),
         "atr_render_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, i64 * 10], C.c_int),
         "atr_render_tile_costs": ([vp, P(atr_camera), vp, i32, C.c_uint64, vp], C.c_int),
+        "atr_render_wave_trace": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp, i64, P(i64)], C.c_int),
         "atr_packed_pixel_map": ([vp, i32, i32, i32, vp, i64], i64),
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
@@ -373,6 +374,16 @@ class Engine:
         check(lib().atr_render_tile_costs(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n,
                                           C.c_uint64(seed & (2**64 - 1)), out.ctypes.data), "tile costs")
         return out[:n]
+
+    def wave_trace(self, cam, tiles, seed, variant=0):
+        """Diagnostic: (nblocks, 3) u64 per work block: start, end (100 MHz), HW_ID | XCC_ID << 32."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        nb = C.c_int64()
+        args = (self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed & (2**64 - 1)), int(variant))
+        check(lib().atr_render_wave_trace(*args, None, 0, C.byref(nb)), "wave trace")
+        out = np.zeros((max(1, nb.value), 3), np.uint64)
+        check(lib().atr_render_wave_trace(*args, out.ctypes.data, out.size, C.byref(nb)), "wave trace")
+        return out[:nb.value]
 
     def wait(self, timeout_ms=0xFFFFFFFF):
         done = C.c_int32()

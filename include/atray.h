@@ -32,6 +32,8 @@ enum {
     ATR_E_NOMEM = -3,
     ATR_E_NOSCENE = -4,     /* render before atr_scene_upload */
     ATR_E_TREE_DEPTH = -5,  /* octree deeper than the traversal's mask stack (16 levels) */
+    ATR_E_TREE_LAYOUT = -6, /* children boxes are not the parent's split-point octants
+                               (build_oct_kd_tree makes them so, kd_tree.cpp:116-148) */
     ATR_E_HIP = -1000       /* -(1000 + hipError_t) */
 };
 
@@ -171,6 +173,11 @@ int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
 /* Load-balance calibration, synchronous: renders `tiles` once (default kernel) and returns the
    GPU shader clocks spent per tile (sum over the 8x8 blocks whose area first falls in the tile,
    list order). Used to deal shard tiles to GPUs by measured cost (atray_amd/shard.py). */
+/* Diagnostic: one render of `tiles` recording, per 8x8 work block (block order), the wave's start
+   and end on the 100 MHz device clock and its HW_ID | XCC_ID << 32. out = 3 u64 per block;
+   with out == NULL (or cap too small) only *nblocks is set. */
+int atr_render_wave_trace(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                          uint64_t seed, int32_t variant, uint64_t* out, int64_t cap, int64_t* nblocks);
 int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                           uint64_t seed, int64_t* cost_out);
 int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,

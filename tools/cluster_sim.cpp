@@ -1,0 +1,250 @@
+// cluster_sim.cpp -- offline work model of the clustered leaf scan (analysis tool, not product).
+//
+// Builds the Dragon surrogate's octree and leaf clusters with the product's host code, traces
+// the primary rays of a 1920x1080 frame (every `step`-th pixel) on the CPU with the reference
+// leaf order (kd_tree.cpp:337-465) and counts, per ray, the work of several leaf-scan
+// strategies: cluster records read, primitives screened, full triangle tests. The strategies
+// differ only in which clusters they read and in which order, never in the result.
+//
+// g++ -O2 -std=c++17 -ffp-contract=off -I atray_amd/csrc tools/cluster_sim.cpp
+//     atray_amd/csrc/host_scene.cpp -o build/cluster_sim && build/cluster_sim OBJ [step]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <vector>
+
+#include "engine.h"
+#include "host_scene.h"
+
+using namespace atr;
+
+static float tri_hit(V3 o, V3 d, V3 a, V3 ab, V3 ac) {
+    const V3 pvec = cross(d, ac);
+    const float det = dot(ab, pvec);
+    if (det < kTol) return 0;
+    const float det_inv = 1 / det;
+    const V3 tvec = sub(o, a);
+    const float u = dot(tvec, pvec) * det_inv;
+    if (u < 0 || u > 1) return 0;
+    const V3 qvec = cross(tvec, ab);
+    const float v = dot(d, qvec) * det_inv;
+    if (v < 0 || u + v > 1) return 0;
+    return dot(qvec, ac) * det_inv;
+}
+
+static float box_entry(V3 o, V3 inv, const float* b) {
+    const int s0 = inv.x < 0, s1 = inv.y < 0, s2 = inv.z < 0;
+    float tmin = ((s0 ? b[3] : b[0]) - o.x) * inv.x, tmax = ((s0 ? b[0] : b[3]) - o.x) * inv.x;
+    const float tymin = ((s1 ? b[4] : b[1]) - o.y) * inv.y, tymax = ((s1 ? b[1] : b[4]) - o.y) * inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return 0;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((s2 ? b[5] : b[2]) - o.z) * inv.z, tzmax = ((s2 ? b[2] : b[5]) - o.z) * inv.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return 0;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    if (tmin > 0) return tmin;
+    if (tmax > 0) return tmax;
+    return 0;
+}
+static bool box_check(V3 o, V3 inv, const float* b) {
+    const int s0 = inv.x < 0, s1 = inv.y < 0, s2 = inv.z < 0;
+    float tmin = ((s0 ? b[3] : b[0]) - o.x) * inv.x, tmax = ((s0 ? b[0] : b[3]) - o.x) * inv.x;
+    const float tymin = ((s1 ? b[4] : b[1]) - o.y) * inv.y, tymax = ((s1 ? b[1] : b[4]) - o.y) * inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((s2 ? b[5] : b[2]) - o.z) * inv.z, tzmax = ((s2 ? b[2] : b[5]) - o.z) * inv.z;
+    return !((tmin > tzmax) || (tzmin > tmax));
+}
+
+struct Stats { double rays = 0, active = 0, leaves = 0, crec = 0, cpass = 0, screen = 0, full = 0, nb_cull = 0; };
+
+int main(int argc, char** argv) {
+    if (argc < 2) { std::fprintf(stderr, "usage: cluster_sim OBJ [step] [cluster]\n"); return 2; }
+    const int step = argc > 2 ? std::atoi(argv[2]) : 2;
+    const int csize = argc > 3 ? std::atoi(argv[3]) : 16;
+    std::ifstream f(argv[1], std::ios::binary);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string text = ss.str();
+    HostMesh M;
+    if (parse_obj_text(text.data(), text.size(), M)) return 1;
+    float box[6];
+    mesh_aabb(M, box);
+    mesh_translate(M, box, mk(0.f, -15.f, -38.f));
+    HostTree T;
+    if (octree_build(M, 300, T)) return 1;
+    LeafClusters C;
+    if (leaf_clusters(T, csize, C)) return 1;
+    const size_t ncl = C.rec.size() / 8;
+    // per-cluster normal box (of the stored n = ab x ac) and centroid
+    std::vector<float> nbox(6 * ncl), cen(3 * ncl);
+    std::vector<uint32_t> cnt(ncl), first(ncl);
+    for (size_t c = 0; c < ncl; ++c) {
+        uint32_t pw, fs;
+        std::memcpy(&pw, &C.rec[8 * c + 3], 4);
+        std::memcpy(&fs, &C.rec[8 * c + 7], 4);
+        cnt[c] = (pw & 31u) + 1u;
+        first[c] = fs;
+        float* nb = &nbox[6 * c];
+        nb[0] = nb[1] = nb[2] = 1e30f;
+        nb[3] = nb[4] = nb[5] = -1e30f;
+        for (uint32_t k = fs; k < fs + cnt[c]; ++k)
+            for (int a = 0; a < 3; ++a) {
+                nb[a] = std::min(nb[a], C.normal[3 * k + a]);
+                nb[3 + a] = std::max(nb[3 + a], C.normal[3 * k + a]);
+            }
+        for (int a = 0; a < 3; ++a) cen[3 * c + a] = 0.5f * (C.rec[8 * c + a] + C.rec[8 * c + 4 + a]);
+    }
+    atr_camera cm;
+    camera_set(cm, mk(0.1f, 2.f, 0.f), mk(-0.1f, -0.5f, -1.f), 1920, 1080, 0, 1, 1, 1.f);
+    const V3 eye = from(cm.eye), fc = from(cm.frame_center), cx = from(cm.camera_x), cy = from(cm.camera_y);
+    enum { NS = 4 };
+    const char* names[NS] = {"kernel (loose+tight pad)", "normal-box det pad", "ideal cluster filter", "normal-box pad + octant"};
+    Stats st[NS];
+    std::vector<std::pair<float, int>> leaves;
+    std::vector<int32_t> stack;
+    // per-pixel work of strategy 0 (step 1 only): leaves, cluster records, screen batches of 4,
+    // full tests, inner nodes visited
+    const char* dump = std::getenv("SIM_DUMP");
+    std::vector<float> pix(dump ? size_t(cm.width) * cm.height * 5 : 0, 0.f);
+    for (int y = 0; y < cm.height; y += step)
+        for (int x = 0; x < cm.width; x += step) {
+            const float film_y = -1.0f + 2.0f * (float(y) / float(cm.height));
+            const float film_x = ((-1.0f + 2.0f * (float(x) / float(cm.width))) * cm.h_fov) * cm.aspect_ratio;
+            const V3 d = unit(sub(add(add(fc, scale(cx, film_x)), scale(cy, film_y)), eye));
+            const V3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+            for (auto& s : st) s.rays += 1;
+            if (!box_check(eye, inv, &T.bounds[0])) continue;
+            // reference DFS: sorted leaf list (stable), nodes_hit <= 4
+            leaves.clear();
+            stack.assign(1, 0);
+            while (!stack.empty()) {
+                const int32_t cur = stack.back();
+                stack.pop_back();
+                if (dump) pix[(size_t(y) * cm.width + x) * 5 + 4] += 1;
+                const int32_t ch = T.children[size_t(cur)];
+                int hit = 0;
+                for (int i = 0; i < 8 && hit <= 4; ++i) {
+                    const int32_t c = ch + i;
+                    if (T.children[size_t(c)]) {
+                        if (box_check(eye, inv, &T.bounds[6 * size_t(c)])) { ++hit; stack.push_back(c); }
+                    } else {
+                        const float dis = box_entry(eye, inv, &T.bounds[6 * size_t(c)]);
+                        if (dis > 0) {
+                            ++hit;
+                            auto it = std::upper_bound(leaves.begin(), leaves.end(), dis,
+                                                       [](float v, const std::pair<float, int>& e) { return v < e.first; });
+                            leaves.insert(it, {dis, c});
+                        }
+                    }
+                }
+            }
+            const int oct = (d.x < 0) * 4 + (d.y < 0) * 2 + (d.z < 0);
+            const float od[3] = {oct & 4 ? -1.f : 1.f, oct & 2 ? -1.f : 1.f, oct & 1 ? -1.f : 1.f};
+            for (int s = 0; s < NS; ++s) {
+                Stats& S = st[s];
+                S.active += 1;
+                float best = kMaxFloat;
+                for (auto& lf : leaves) {
+                    S.leaves += 1;
+                    if (dump && s == 0) pix[(size_t(y) * cm.width + x) * 5 + 0] += 1;
+                    const uint32_t c0 = C.range[2 * size_t(lf.second)], nc = C.range[2 * size_t(lf.second) + 1];
+                    std::vector<uint32_t> ord(nc);
+                    for (uint32_t k = 0; k < nc; ++k) ord[k] = c0 + k;
+                    if (s == 3)
+                        std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+                            const float pa = cen[3 * a] * od[0] + cen[3 * a + 1] * od[1] + cen[3 * a + 2] * od[2];
+                            const float pb = cen[3 * b] * od[0] + cen[3 * b + 1] * od[1] + cen[3 * b + 2] * od[2];
+                            return pa < pb;
+                        });
+                    bool improved = false;
+                    for (uint32_t c : ord) {
+                        S.crec += 1;
+                        if (dump && s == 0) pix[(size_t(y) * cm.width + x) * 5 + 1] += 1;
+                        const float* r = &C.rec[8 * size_t(c)];
+                        // rounding-padded cluster box for a det lower bound D (render.hip
+                        // scan_leaf_clusters): g = W (36 eps P / (0.9 D) + 12 eps)
+                        const float eps = 5.9604645e-8f, tau = 3e-3f;
+                        const float ex = r[4] - r[0], ey = r[5] - r[1], ez = r[6] - r[2];
+                        const float fx = std::max(std::fabs(r[0] - eye.x), std::fabs(r[4] - eye.x));
+                        const float fy = std::max(std::fabs(r[1] - eye.y), std::fabs(r[5] - eye.y));
+                        const float fz = std::max(std::fabs(r[2] - eye.z), std::fabs(r[6] - eye.z));
+                        const float W = std::sqrt(fx * fx + fy * fy + fz * fz) * 1.0000005f + (ex + ey + ez);
+                        const float P = r[3];
+                        auto pad = [&](float D) { return W * (P * (36 * eps / (0.9f * D)) + 12 * eps); };
+                        auto hitbox = [&](float g) {
+                            float bb[6];
+                            for (int q = 0; q < 3; ++q) { bb[q] = r[q] - g; bb[3 + q] = r[4 + q] + g; }
+                            return box_check(eye, inv, bb) && !(box_entry(eye, inv, bb) > best);
+                        };
+                        const float mg = 16 * eps * P;
+                        float dlo = kTol - mg, dhi = 1e30f;
+                        const float* nb = &nbox[6 * c];
+                        float lb = 0.f, ub = 0.f, mag = 0.f;
+                        for (int q = 0; q < 3; ++q) {
+                            const float da = (&d.x)[q];
+                            lb += std::min(-da * nb[q], -da * nb[3 + q]);
+                            ub += std::max(-da * nb[q], -da * nb[3 + q]);
+                            mag += std::fabs(da) * std::max(std::fabs(nb[q]), std::fabs(nb[3 + q]));
+                        }
+                        lb -= 8 * eps * mag + mg;
+                        ub += 8 * eps * mag;
+                        bool perprim = false;
+                        if (s == 0) {  // the kernel: loose + tight box
+                            if (!hitbox(pad(kTol))) continue;
+                            if (!hitbox(pad(tau))) dhi = tau + mg;
+                        } else if (s == 1 || s == 3) {  // normal-box det bound sets the pad
+                            if (ub < dlo) { S.nb_cull += 1; continue; }
+                            if (!hitbox(pad(std::max(lb, kTol)))) continue;
+                            perprim = true;
+                        } else {  // ideal: a cluster is read only if one of its prims needs a test
+                            if (ub < dlo) { S.nb_cull += 1; continue; }
+                            bool any = false;
+                            for (uint32_t k = first[c]; k < first[c] + cnt[c] && !any; ++k) {
+                                const float* n = &C.normal[3 * k];
+                                const float det = -(d.x * n[0] + d.y * n[1] + d.z * n[2]);
+                                any = det >= dlo && hitbox(pad(std::max(det - mg, kTol)));
+                            }
+                            if (!any) continue;
+                            perprim = true;
+                        }
+                        S.cpass += 1;
+                        if (dump && s == 0) pix[(size_t(y) * cm.width + x) * 5 + 2] += float((cnt[c] + 3) / 4);
+                        for (uint32_t k = first[c]; k < first[c] + cnt[c]; ++k) {
+                            S.screen += 1;
+                            const float* n = &C.normal[3 * k];
+                            const float det = -(d.x * n[0] + d.y * n[1] + d.z * n[2]);
+                            if (!(det >= dlo && det < dhi)) continue;
+                            if (perprim && !hitbox(pad(std::max(det - mg, kTol)))) continue;
+                            S.full += 1;
+                            if (dump && s == 0) pix[(size_t(y) * cm.width + x) * 5 + 3] += 1;
+                            const float* v = &T.prim_vertices[9 * size_t(C.order[k])];
+                            const V3 a = mk(v[0], v[1], v[2]);
+                            const float t = tri_hit(eye, d, a, sub(mk(v[3], v[4], v[5]), a), sub(mk(v[6], v[7], v[8]), a));
+                            if (t > kTol && t < best) { best = t; improved = true; }
+                        }
+                    }
+                    if (improved) break;
+                }
+            }
+        }
+    if (dump) {
+        FILE* o = std::fopen(dump, "wb");
+        std::fwrite(pix.data(), sizeof(float), pix.size(), o);
+        std::fclose(o);
+    }
+    std::printf("clusters %zu (size %d), rays %.0f, active %.0f\n", ncl, csize, st[0].rays, st[0].active);
+    for (int s = 0; s < NS; ++s) {
+        const Stats& S = st[s];
+        const double a = S.active;
+        std::printf("%-28s per active ray: leaves %.2f  cluster recs %.1f  boxes passed %.1f  normal-culled %.1f  screens %.1f  full tests %.1f\n",
+                    names[s], S.leaves / a, S.crec / a, S.cpass / a, S.nb_cull / a, S.screen / a, S.full / a);
+    }
+    return 0;
+}
