@@ -19,6 +19,7 @@
 using namespace atr;
 
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s);
+extern "C" hipError_t atr_launch_persist(const atr::RenderParams& P, int ncu, hipStream_t s);
 extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                         const uint32_t* packed, uint32_t* image, hipStream_t s);
 extern "C" hipError_t atr_wf_render(const atr::WFParams& W, int32_t nmodels, const int32_t* nnodes,
@@ -99,10 +100,24 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     }
 }
 
-int32_t xcd_chunk() {  // EXPERIMENT knob (ATR_XCD_CHUNK), read once
-    static const int32_t v = [] { const char* e = std::getenv("ATR_XCD_CHUNK"); return e ? std::atoi(e) : 0; }();
+int32_t env_int(const char* name, int32_t dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+// 8x8-cell schedules: workgroup chunks dealt round-robin to the XCDs (render.hip remap_xcd;
+// DESIGN.md §4c). ATR_XCD_CHUNK overrides (0 = one contiguous range per XCD).
+int32_t xcd_chunk() {
+    static const int32_t v = env_int("ATR_XCD_CHUNK", 16);
     return v;
 }
+// PERSIST: 8x8 cells per work-queue chunk (ATR_QCHUNK overrides).
+int32_t qchunk() {
+    static const int32_t v = std::max(1, env_int("ATR_QCHUNK", 16));
+    return v;
+}
+constexpr int kSchedPersist = 8;
+constexpr int kQueueSlots = 32;             // queue-head sets in flight (ring)
+constexpr size_t kQueueBytes = 8 * 32 * 4;  // 8 heads, 128 B apart
 
 }  // namespace
 
@@ -130,6 +145,13 @@ struct atr_ctx {
     atr::WFParams wf = {};
     int32_t* wf_pinned = nullptr;
     std::vector<int32_t> model_nodes, model_tree;
+    // PERSIST work-queue heads: a ring of sets, each zeroed on the launch stream before use and
+    // reused only after the launch that last used it (event) has finished
+    int ncu = 256;
+    void* qring = nullptr;
+    hipEvent_t qev[kQueueSlots] = {};
+    bool qused[kQueueSlots] = {};
+    int qnext = 0;
 };
 
 namespace {
@@ -283,9 +305,28 @@ int sched_of(int32_t variant) {
         case ATR_KERNEL_TILE: return 2;
         case ATR_KERNEL_TILE8: return 3;
         case ATR_KERNEL_CLUSTER: return 4;
+        case ATR_KERNEL_PERSIST: return kSchedPersist;
         case ATR_KERNEL_AUTO: return 4;  // CLUSTER: fastest measured
         default: return variant >= 16 ? variant : 0;
     }
+}
+
+// Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
+hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
+    if (sched != kSchedPersist) return atr_launch_render(P, sched, s);
+    if (P.nblocks <= 0) return hipSuccess;
+    const int k = c->qnext;
+    c->qnext = (k + 1) % kQueueSlots;
+    uint32_t* q = reinterpret_cast<uint32_t*>(static_cast<char*>(c->qring) + size_t(k) * kQueueBytes);
+    hipError_t e;
+    if (c->qused[k] && (e = hipStreamWaitEvent(s, c->qev[k], 0)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(q, 0, kQueueBytes, s)) != hipSuccess) return e;
+    P.queue = q;
+    P.qchunk = qchunk();
+    if ((e = atr_launch_persist(P, c->ncu, s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(c->qev[k], s)) != hipSuccess) return e;
+    c->qused[k] = true;
+    return hipSuccess;
 }
 
 }  // namespace
@@ -447,6 +488,10 @@ int atr_create(int device, atr_ctx** out) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
     HIPCHK(hipMalloc(&c->d_error, 16));
     HIPCHK(hipMemset(c->d_error, 0, 16));
+    HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipMalloc(&c->qring, kQueueSlots * kQueueBytes));
+    HIPCHK(hipMemset(c->qring, 0, kQueueSlots * kQueueBytes));
+    for (hipEvent_t& e : c->qev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
     return ATR_OK;
 }
@@ -464,6 +509,9 @@ int atr_destroy(atr_ctx* c) {
     if (c->wf_mem.p) (void)hipFree(c->wf_mem.p);
     if (c->wf_pinned) (void)hipHostFree(c->wf_pinned);
     if (c->d_error) (void)hipFree(c->d_error);
+    if (c->qring) (void)hipFree(c->qring);
+    for (hipEvent_t e : c->qev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev_start);
     (void)hipEventDestroy(c->ev_stop);
     (void)hipEventDestroy(c->ev_done);
@@ -782,7 +830,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.xcd_chunk = xcd_chunk();
     const int wave = sched_of(variant);
     HIPCHK(hipEventRecord(c->ev_start, s));
-    HIPCHK(atr_launch_render(P, wave, s));
+    HIPCHK(launch_render(c, P, wave, s));
     HIPCHK(hipEventRecord(c->ev_stop, s));
     HIPCHK(hipEventRecord(c->ev_done, s));
     c->have_render = true;
@@ -818,7 +866,8 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.error_flag = c->d_error;
     P.wave_trace = static_cast<unsigned long long*>(tr);
     P.xcd_chunk = xcd_chunk();
-    HIPCHK(atr_launch_render(P, sched_of(variant), nullptr));
+    const int ts = sched_of(variant);  // per-cell trace: 8x8-cell schedules only
+    HIPCHK(atr_launch_render(P, ts == kSchedPersist ? 4 : ts, nullptr));
     HIPCHK(hipDeviceSynchronize());
     if (nb) HIPCHK(hipMemcpy(out, tr, 3 * nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     HIPCHK(hipFree(fb));
@@ -851,7 +900,7 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.error_flag = c->d_error;
     P.counters = static_cast<unsigned long long*>(ctr);
     const int sc = sched_of(variant);
-    HIPCHK(atr_launch_render(P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
+    HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
     unsigned long long h[10];
     HIPCHK(hipMemcpy(h, ctr, sizeof(h), hipMemcpyDeviceToHost));
@@ -885,7 +934,8 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.framebuffer = static_cast<uint32_t*>(fb);
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost);
-    HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_AUTO), nullptr));
+    P.xcd_chunk = xcd_chunk();
+    HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_CLUSTER), nullptr));  // per-cell clocks
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
     if (nb) HIPCHK(hipMemcpy(h.data(), cost, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));

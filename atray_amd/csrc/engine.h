@@ -165,6 +165,8 @@ struct RenderParams {
     unsigned long long* block_cost;  // non-null -> shader clocks spent per block (load balance)
     unsigned long long* wave_trace;  // non-null -> per block: start, end (100 MHz clock), HW_ID | XCC_ID << 32
     int32_t xcd_chunk;  // 0: contiguous block range per XCD; k > 0: k-workgroup chunks dealt round-robin
+    uint32_t* queue;    // PERSIST: 8 zeroed per-XCD work-queue heads (persist.hip)
+    int32_t qchunk;     // PERSIST: 8x8 cells per queue chunk
 };
 
 }  // namespace atr

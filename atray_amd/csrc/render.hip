@@ -11,20 +11,11 @@
 //         in its own order, so results are identical.
 #include <hip/hip_runtime.h>
 
+#include "cluster.h"
+#include "shade.h"
 #include "trace.h"
 
 namespace atr {
-
-enum { T_NONE = 0, T_TRI = 1, T_SPHERE = 2, T_PLANE = 3, T_SKY = 4 };
-
-struct Isect {
-    int type;
-    float t;
-    V3 normal;
-    int32_t material;
-    uint32_t face;
-};
-
 
 // ------------------------------------------------------------------ LANE schedule
 // Per-lane leaf scan over the SoA triangle streams, one triangle of prefetch: the loads of
@@ -77,122 +68,33 @@ __device__ __forceinline__ bool scan_leaf_lane(const Ray& r, const DModel& m, ui
 }
 
 // ------------------------------------------------------------------ clustered leaf scan
-// The same leaf result from a fraction of the triangle tests. Each leaf's
-// primitives are regrouped into spatial clusters of <= 16 with a bounding box, and a primitive
-// is skipped only when it provably cannot be accepted with t <= the best so far:
-//   * rounding (first order): an accepted hit of the culled test (computed
-//     det >= kTol; u, v in range) has its true line within D_lat of the triangle and its
-//     computed t within D_t of the true t, D_lat + D_t <= W (29 eps |ab||ac| / det + 6 eps),
-//     W >= |o - a| + |edge|: the u, v, t numerators carry ~7.5 eps |tvec| |ac| (resp. |ab|,
-//     |ab||ac|) of cancellation, det ~6.5 eps |ab||ac|. A box grown by that much (36 and
-//     12 eps here, with the slab's own rounding) is entered no later than the computed t of any
-//     acceptable primitive inside and left no earlier.
-//   * D depends on det, which is not known per cluster: the box is grown twice, for det >= kTol
-//     (loose) and det >= kTau (tight). Missing the loose box skips the cluster. Inside the
-//     tight box every front-facing primitive is a candidate. In between, only primitives whose
-//     det could lie in [kTol, kTau) are: the det estimate -(d . n) (n = ab x ac, one 16-B
-//     load) is within 16 eps |ab||ac| of the computed det, which sets the screen's margins.
-//     Back-facing primitives (det < kTol) are screened out the same way in both cases.
-//   * inside the leaf the reference keeps the FIRST primitive (leaf order) with the smallest t
-//     below the incoming best (strict <, kd_tree.cpp:440-456); clusters change the visiting
-//     order, so equal t is resolved by the leaf rank, and a best carried in from an earlier
-//     leaf never loses a tie.
-constexpr float kTau = 3e-3f;
-constexpr float kEps = 5.9604645e-8f;  // 2^-24
-constexpr float kPadRel = 36.0f * kEps, kPadAbs = 12.0f * kEps;
-
-template <bool COUNT>
-__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, float acz, float& best_t,
-                                            uint32_t& best_slot, float& bu, float& bv, int32_t& brank,
-                                            bool& improved, Ctr& ct) {
-    if constexpr (COUNT) ct.tri += 1;
-    const float4_t q0 = m.c0[k], q1 = m.c1[k];
-    float u = 0.f, v = 0.f;
-    const float dist = tri_hit(r, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, acz), u, v);
-    if (dist <= best_t && dist > kTol) {
-        const int32_t rk = int32_t(m.crank[k]);
-        if (dist < best_t || (brank >= 0 && rk < brank)) {
-            best_t = dist;
-            best_slot = k;
-            bu = u;
-            bv = v;
-            brank = rk;
-            improved = true;
-        }
-    }
-}
-
+// One leaf over its clusters (cluster.h), the next cluster's record in flight while the current
+// one is screened.
 template <bool COUNT>
 __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m, uint32_t cfirst,
                                                    uint32_t ccount, float& best_t, uint32_t& best_slot,
                                                    float& bu, float& bv, Ctr& ct) {
     if constexpr (COUNT) { ct.leaf += 1; ct.cbox += ccount; }
-    bool improved = false;
-    int32_t brank = -1;
+    LeafHit h;
+    h.t = best_t;
+    h.slot = best_slot;
+    h.u = bu;
+    h.v = bv;
+    h.rank = -1;
+    h.improved = false;
     const uint32_t cend = cfirst + ccount;
-    const float ax = fabsf(r.inv.x), ay = fabsf(r.inv.y), az = fabsf(r.inv.z);
-    float4_t nlo, nhi;  // next cluster's record, in flight while this one is screened
+    float4_t nlo, nhi;
     if (ccount) { nlo = m.clus[2 * cfirst]; nhi = m.clus[2 * cfirst + 1]; }
     for (uint32_t c = cfirst; c < cend; ++c) {
         const float4_t lo = nlo, hi = nhi;
         if (c + 1 < cend) { nlo = m.clus[2 * c + 2]; nhi = m.clus[2 * c + 3]; }
-        const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
-        const float fx = fmaxf(fabsf(lo.x - r.o.x), fabsf(hi.x - r.o.x));
-        const float fy = fmaxf(fabsf(lo.y - r.o.y), fabsf(hi.y - r.o.y));
-        const float fz = fmaxf(fabsf(lo.z - r.o.z), fabsf(hi.z - r.o.z));
-        // W >= |o - a| + |edge| for every primitive inside (far corner; L1 extent >= diagonal)
-        const float W = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0000005f + (ex + ey + ez);
-        const float P = lo.w;  // >= |ab||ac| of every primitive inside
-        const float gl = W * (P * (kPadRel / (0.9f * kTol)) + kPadAbs);
-        const float gt = W * (P * (kPadRel / (0.9f * kTau)) + kPadAbs);
-        // slab entry/exit of the unpadded box per axis, then widened by g |inv| per axis
-        const float x0 = (lo.x - r.o.x) * r.inv.x, x1 = (hi.x - r.o.x) * r.inv.x;
-        const float y0 = (lo.y - r.o.y) * r.inv.y, y1 = (hi.y - r.o.y) * r.inv.y;
-        const float z0 = (lo.z - r.o.z) * r.inv.z, z1 = (hi.z - r.o.z) * r.inv.z;
-        const float nx = fminf(x0, x1), fx1 = fmaxf(x0, x1), ny = fminf(y0, y1), fy1 = fmaxf(y0, y1),
-                    nz = fminf(z0, z1), fz1 = fmaxf(z0, z1);
-        float tn = fmaxf(fmaxf(nx - gl * ax, ny - gl * ay), nz - gl * az);
-        float tf = fminf(fminf(fx1 + gl * ax, fy1 + gl * ay), fz1 + gl * az);
-        if (tn > tf || tf < 0.f || tn > best_t) continue;
-        tn = fmaxf(fmaxf(nx - gt * ax, ny - gt * ay), nz - gt * az);
-        tf = fminf(fminf(fx1 + gt * ax, fy1 + gt * ay), fz1 + gt * az);
-        const bool tight = !(tn > tf || tf < 0.f || tn > best_t);
-#ifdef ATR_EXP_SKIP_LOOSE
-        if (!tight) continue;  // EXPERIMENT ONLY (not exact): cost of the loose-only screens
-#endif
-        const float mg = 16.0f * kEps * P;
-        const float dlo = kTol - mg, dhi = tight ? __builtin_inff() : kTau + mg;
-        const uint32_t first = __float_as_uint(hi.w);
-        const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u, last = first + n - 1;
-        if constexpr (COUNT) ct.screen += n;
-        // screen four primitives per step (their normal loads in flight together)
-        for (uint32_t k = first; k <= last; k += 4) {
-            const uint32_t k1 = k + 1 <= last ? k + 1 : last, k2 = k + 2 <= last ? k + 2 : last,
-                           k3 = k + 3 <= last ? k + 3 : last;
-            const float4_t n0 = m.c2[k], n1 = m.c2[k1], n2 = m.c2[k2], n3 = m.c2[k3];
-            const float d0 = -(r.d.x * n0.x + r.d.y * n0.y + r.d.z * n0.z);
-            const float d1 = -(r.d.x * n1.x + r.d.y * n1.y + r.d.z * n1.z);
-            const float d2 = -(r.d.x * n2.x + r.d.y * n2.y + r.d.z * n2.z);
-            const float d3 = -(r.d.x * n3.x + r.d.y * n3.y + r.d.z * n3.z);
-            if (d0 >= dlo && d0 < dhi) cluster_tri<COUNT>(r, m, k, n0.w, best_t, best_slot, bu, bv, brank, improved, ct);
-            if (k + 1 <= last && d1 >= dlo && d1 < dhi)
-                cluster_tri<COUNT>(r, m, k + 1, n1.w, best_t, best_slot, bu, bv, brank, improved, ct);
-            if (k + 2 <= last && d2 >= dlo && d2 < dhi)
-                cluster_tri<COUNT>(r, m, k + 2, n2.w, best_t, best_slot, bu, bv, brank, improved, ct);
-            if (k + 3 <= last && d3 >= dlo && d3 < dhi)
-                cluster_tri<COUNT>(r, m, k + 3, n3.w, best_t, best_slot, bu, bv, brank, improved, ct);
-        }
+        cluster_step<COUNT>(r, m, lo, hi, h, ct);
     }
-    return improved;
-}
-
-// Sorted-leaf scan with a rotating head: entry 0 is always the next leaf, the buffer shifts
-// down after each scanned leaf (static register moves, no dynamically indexed arrays).
-template <int K>
-__device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
-#pragma unroll
-    for (int j = 0; j + 1 < K; ++j) { b.d[j] = b.d[j + 1]; b.node[j] = b.node[j + 1]; b.idx[j] = b.idx[j + 1]; }
-    b.d[K - 1] = __builtin_inff();
+    best_t = h.t;
+    best_slot = h.slot;
+    bu = h.u;
+    bv = h.v;
+    return h.improved;
 }
 
 template <bool COUNT, bool CL = false, int K = kLeafBuf>
@@ -484,7 +386,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                                                 Isect& id, int& err, Ctr& ct) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
     float best = kMaxFloat;
-    int32_t nm = -1, ns = -1, np = -1;
+    int32_t nm = -1;
     uint32_t face = 0;
     float fu = 0.f, fv = 0.f;
     const int32_t nmodels = S->nmodels;
@@ -521,62 +423,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
         }
     }
     if (!active) return;
-    for (int32_t i = 0; i < S->nspheres; ++i) {  // sphere.h:12-39
-        const DSphere& sp = S->spheres[i];
-        const V3 pc = sub(o, mk(sp.cx, sp.cy, sp.cz));
-        const float pcs = len2(pc);
-        const float b = 2 * (dot(d, pc));
-        const float bs = b * b;
-        const float c = pcs - sp.r * sp.r;
-        const float dmt = bs - (4 * c);
-        float t = 0;
-        if (!(dmt < 0)) {
-            const float ta = (-b + sqrtf(dmt)) * 0.5f;
-            const float tb = (-b - sqrtf(dmt)) * 0.5f;
-            if (ta <= 0 && tb <= 0) t = 0;
-            else if (tb > 0) t = tb;
-            else t = ta;
-        }
-        if (t > kTol && t < best) { best = t; ns = i; }
-    }
-    for (int32_t i = 0; i < S->nplanes; ++i) {  // plane.h:12-22
-        const DPlane& pl = S->planes[i];
-        const V3 n = mk(pl.nx, pl.ny, pl.nz);
-        const float denom = dot(n, d);
-        float t = 0;
-        if (!(denom > -kTol && denom < kTol)) t = (pl.d - dot(o, n)) / denom;
-        if (t > kTol && t < best) { np = i; best = t; }
-    }
-    id.t = best;
-    id.face = 0xFFFFFFFFu;
-    if (np >= 0) {
-        const DPlane& pl = S->planes[np];
-        id.type = T_PLANE;
-        id.normal = mk(pl.nx, pl.ny, pl.nz);
-        id.material = pl.material;
-    } else if (ns >= 0) {
-        const DSphere& sp = S->spheres[ns];
-        id.type = T_SPHERE;
-        id.normal = sub(add(o, scale(d, best)), mk(sp.cx, sp.cy, sp.cz));  // Ray::at (ray.h:10-13)
-        id.material = sp.material;
-    } else if (nm >= 0) {
-        const DModel& m = S->models[nm];
-        id.type = T_TRI;
-        id.face = face;
-        const float* sh = m.shade + 9 * size_t(face);
-        if (m.smooth) {  // interpolated vertex normals (:129-138)
-            const V3 na = mk(sh[0], sh[1], sh[2]), nb = mk(sh[3], sh[4], sh[5]), nc = mk(sh[6], sh[7], sh[8]);
-            id.normal = add(add(scale(na, (1 - fu - fv)), scale(nb, fu)), scale(nc, fv));
-        } else {  // flat (:140-146)
-            const V3 v0 = mk(sh[0], sh[1], sh[2]), v1 = mk(sh[3], sh[4], sh[5]), v2 = mk(sh[6], sh[7], sh[8]);
-            id.normal = cross(sub(v0, v1), sub(v0, v2));
-        }
-        id.material = m.material;
-    } else {
-        id.type = T_SKY;
-        id.material = 0;
-    }
-    if (id.type != T_SKY) id.normal = unit(id.normal);  // :157
+    scene_finish(S, o, d, best, face, fu, fv, nm, id);  // :86-160
 }
 
 // ------------------------------------------------------------------ cast_ray + pixel loop

@@ -177,6 +177,15 @@ __device__ __forceinline__ void lb_insert(LeafBuf<K>& b, float dis, int32_t node
     }
 }
 
+// Sorted-leaf scan with a rotating head: entry 0 is always the next leaf, the buffer shifts
+// down after each scanned leaf (static register moves, no dynamically indexed arrays).
+template <int K>
+__device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
+#pragma unroll
+    for (int j = 0; j + 1 < K; ++j) { b.d[j] = b.d[j + 1]; b.node[j] = b.node[j + 1]; b.idx[j] = b.idx[j + 1]; }
+    b.d[K - 1] = __builtin_inff();
+}
+
 template <int K>
 __device__ __forceinline__ int32_t lb_node(const LeafBuf<K>& b, int j) {
     int32_t r = b.node[0];

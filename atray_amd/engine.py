@@ -22,6 +22,7 @@ ATR_LAYOUT_PACKED = 1
 ATR_KERNEL_AUTO, ATR_KERNEL_LANE, ATR_KERNEL_WAVE, ATR_KERNEL_TILE, ATR_KERNEL_TILE8 = 0, 1, 2, 3, 4
 ATR_KERNEL_WAVEFRONT = 5
 ATR_KERNEL_CLUSTER = 6
+ATR_KERNEL_PERSIST = 7
 MISS = 0xFFFFFFFF
 MAX_FLOAT = np.float32(3.402823466e38)
 

@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl"])
+    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps"])
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -157,7 +157,8 @@ def main():
     asset, W, H, spp, bounces, use_tree = CONFIGS[args.config]
     variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE,
                "tile": E.ATR_KERNEL_TILE, "tile8": E.ATR_KERNEL_TILE8,
-               "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER}[args.variant]
+               "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
+               "ps": E.ATR_KERNEL_PERSIST}[args.variant]
     mesh = E.Mesh.load_obj(asset_path(asset))
     box = mesh.translate_to(mesh.aabb(), CENTERS[asset])
     tree = E.Octree.build(mesh, 300) if use_tree else None
@@ -301,7 +302,7 @@ def main():
             out["check_mismatched_pixels"] = check
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
-        clustered = args.variant in ("auto", "cl")
+        clustered = args.variant in ("auto", "cl", "ps")
         if clustered:
             bpr = cluster_bytes_per_ray(live_ctr)
         else:

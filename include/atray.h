@@ -154,7 +154,8 @@ typedef struct {
 
 /* Kernel variant: AUTO picks the fastest exact variant. All variants are bit-identical. */
 enum { ATR_KERNEL_AUTO = 0, ATR_KERNEL_LANE = 1, ATR_KERNEL_WAVE = 2, ATR_KERNEL_TILE = 3,
-       ATR_KERNEL_TILE8 = 4, ATR_KERNEL_WAVEFRONT = 5, ATR_KERNEL_CLUSTER = 6 };
+       ATR_KERNEL_TILE8 = 4, ATR_KERNEL_WAVEFRONT = 5, ATR_KERNEL_CLUSTER = 6,
+       ATR_KERNEL_PERSIST = 7 /* persistent waves, lanes refilled from per-XCD work queues */ };
 
 /* start_render_from_camera: renders the pixels of `tiles` (inclusive rects; overlapping pixels
    are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the null stream, HIP's convention). RNG: deterministic per-pixel PCG stream from `seed` (DESIGN.md "RNG"). Returns
@@ -173,15 +174,15 @@ int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
 /* Load-balance calibration, synchronous: renders `tiles` once (default kernel) and returns the
    GPU shader clocks spent per tile (sum over the 8x8 blocks whose area first falls in the tile,
    list order). Used to deal shard tiles to GPUs by measured cost (atray_amd/shard.py). */
+int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                          uint64_t seed, int64_t* cost_out);
+int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                        uint64_t seed, int32_t variant, int64_t counters_out[10]);
 /* Diagnostic: one render of `tiles` recording, per 8x8 work block (block order), the wave's start
    and end on the 100 MHz device clock and its HW_ID | XCC_ID << 32. out = 3 u64 per block;
    with out == NULL (or cap too small) only *nblocks is set. */
 int atr_render_wave_trace(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                           uint64_t seed, int32_t variant, uint64_t* out, int64_t cap, int64_t* nblocks);
-int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                          uint64_t seed, int64_t* cost_out);
-int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                        uint64_t seed, int32_t variant, int64_t counters_out[10]);
 /* Number of pixels a PACKED render of these tiles writes. */
 int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles);
 /* Host-only: pixel index (y * width + x) of every slot of a PACKED render of these tiles, in

@@ -15,7 +15,7 @@ from tests.goldens import GOLD, SEED, hits, render  # noqa: E402
 pytestmark = pytest.mark.gpu
 SKY, MODEL = O.SKY, O.MODEL_MAT
 VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8,
-            E.ATR_KERNEL_WAVEFRONT, E.ATR_KERNEL_CLUSTER]
+            E.ATR_KERNEL_WAVEFRONT, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST]
 RGB_RTOL = 1e-5
 
 
@@ -244,7 +244,7 @@ def test_gpu_work_counters_equal_reference_work(eng, name, variant):
     c = eng.counters(E.camera(g["W"], g["H"]), [[0, 0, g["W"] - 1, g["H"] - 1]], SEED, variant)
     for k in ["n_rays", "n_box", "n_leaf"]:
         assert c[k] == g["counters"][k], (k, c[k], g["counters"][k])
-    if variant == E.ATR_KERNEL_CLUSTER and g["tree"]:
+    if variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST) and g["tree"]:
         # the clustered scan visits the same leaves but skips provably irrelevant triangles
         assert 0 < c["n_tri"] <= g["counters"]["n_tri"], (c["n_tri"], g["counters"]["n_tri"])
     else:

@@ -44,12 +44,13 @@ def main():
     fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, None, None)
     stream = torch.cuda.current_stream().cuda_stream
     names = {"lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE, "tile": E.ATR_KERNEL_TILE,
-             "tile8": E.ATR_KERNEL_TILE8, "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER, "occ4": 20, "occ5": 21,
+             "tile8": E.ATR_KERNEL_TILE8, "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
+             "ps": E.ATR_KERNEL_PERSIST, "occ4": 20, "occ5": 21,
              "occ6": 22, "occ8": 24, "cl4": 36, "cl5": 37, "cl6": 38, "cl8": 40,
              "k4o4": 52, "k4o5": 53, "k4o6": 54, "k4o8": 56}
     vs = args.variants.split(",")
     res = {v: [] for v in vs}
-    ctrs = {v: eng.counters(cam, tiles, SEED, names[v] if names[v] in (1, 2, 3, 4, 6) else (E.ATR_KERNEL_CLUSTER if names[v] >= 32 else E.ATR_KERNEL_LANE)) for v in vs}
+    ctrs = {v: eng.counters(cam, tiles, SEED, names[v] if names[v] in (1, 2, 3, 4, 6, 7) else (E.ATR_KERNEL_CLUSTER if names[v] >= 32 else E.ATR_KERNEL_LANE)) for v in vs}
     for v in vs:  # warm
         eng.render_start(cam, tiles, fr, SEED, stream=stream, variant=names[v])
     torch.cuda.synchronize()
