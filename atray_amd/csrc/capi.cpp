@@ -2,7 +2,9 @@
 // launches on a HIP stream, progress/wait, and the host prerequisites behind opaque handles.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -132,7 +134,7 @@ struct atr_ctx {
     DScene* d_scene = nullptr;
     int64_t scene_bytes = 0;
     int32_t max_nodes = 0, max_depth = 0, nmodels = 0, max_inner = 0;
-    int cluster_size = 16;     // primitives per leaf cluster (ATR_CLUSTER_SIZE overrides, 1..32)
+    int cluster_size = 16;     // primitives per leaf cluster (ATR_CLUSTER_SIZE overrides, 1..16)
     int64_t nclusters = 0;
     static constexpr int kBlockSlots = 24;  // tile-list cache: own render + one unpack per rank
     BlockSet blocks[kBlockSlots];
@@ -306,9 +308,16 @@ int sched_of(int32_t variant) {
         case ATR_KERNEL_TILE8: return 3;
         case ATR_KERNEL_CLUSTER: return 4;
         case ATR_KERNEL_PERSIST: return kSchedPersist;
-        case ATR_KERNEL_AUTO: return 4;  // CLUSTER: fastest measured
+        case ATR_KERNEL_AUTO: return 4;  // see auto_sched
         default: return variant >= 16 ? variant : 0;
     }
+}
+
+// AUTO: the fastest exact schedule for the camera (measured): primary-only renders
+// (bounce_limit 1, no AA) on 8x8 cells (CLUSTER), multi-bounce paths on PERSIST.
+int auto_sched(int32_t variant, const atr_camera& cam) {
+    if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
+    return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_CLUSTER) : kSchedPersist;
 }
 
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
@@ -552,7 +561,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
     c->nclusters = 0;
     if (const char* e = std::getenv("ATR_CLUSTER_SIZE")) {
         const int v = std::atoi(e);
-        if (v >= 1 && v <= 32) c->cluster_size = v;
+        if (v >= 1 && v <= kMaxClusterSize) c->cluster_size = v;
     }
     for (int32_t i = 0; i < nmodels; ++i) {
         const atr_model& md = models[i];
@@ -637,23 +646,54 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
             {  // clustered copy of the leaf primitives
                 LeafClusters C;
                 if ((rc = leaf_clusters(T, c->cluster_size, C))) return rc;
-                const size_t ns = C.order.size() ? C.order.size() : 1;
-                std::vector<float4_t> s0(ns), s1(ns);
-                std::vector<float4_t> s2(ns);
-                std::vector<uint32_t> sf(ns, 0u), sr(ns, 0u);
-                for (size_t k = 0; k < C.order.size(); ++k) {
-                    const DTri& t = tris[C.order[k]];
-                    s0[k] = float4_t{t.ax, t.ay, t.az, t.abx};
-                    s1[k] = float4_t{t.aby, t.abz, t.acx, t.acy};
-                    s2[k] = float4_t{C.normal[3 * k], C.normal[3 * k + 1], C.normal[3 * k + 2], t.acz};
-                    sf[k] = t.face;
-                    sr[k] = C.rank[k];
+                // every cluster owns kMaxClusterSize consecutive slots (its first slot is 16 c), so
+                // the record's last word can carry the screen normals' step instead
+                const size_t ncl = C.rec.size() / 8;
+                const size_t ns = std::max<size_t>(1, ncl) * kMaxClusterSize;
+                std::vector<float4_t> s0(ns, float4_t{0.f, 0.f, 0.f, 0.f}), s1(ns, float4_t{0.f, 0.f, 0.f, 0.f});
+                std::vector<float4_t> s2(ns, float4_t{0.f, 0.f, 0.f, 0.f});
+                std::vector<uint32_t> sf(ns, 0u);
+                std::vector<uint32_t> nw(ns, 0u);  // 16 packed normals per cluster
+                for (size_t cl = 0; cl < ncl; ++cl) {
+                    uint32_t pw, first;
+                    std::memcpy(&pw, &C.rec[8 * cl + 3], 4);
+                    std::memcpy(&first, &C.rec[8 * cl + 7], 4);
+                    const uint32_t n = (pw & 31u) + 1u;
+                    if (n > uint32_t(kMaxClusterSize)) return ATR_E_INVALID;
+                    // screen normals: a step q >= max |n component| / 511 and each normal as
+                    // round(n / q) in 3 x 10 bits (|n - q * packed| <= q / 2 per component)
+                    double mx = 0.0;
+                    for (uint32_t k = first; k < first + n; ++k)
+                        for (int a = 0; a < 3; ++a) mx = std::max(mx, std::fabs(double(C.normal[3 * k + a])));
+                    float q = float(mx / 511.0);
+                    while (double(q) * 511.0 < mx) q = std::nextafter(q, INFINITY);
+                    if (!(q > 0.f)) q = 1e-30f;
+                    C.rec[8 * cl + 7] = q;
+                    for (uint32_t i = 0; i < n; ++i) {
+                        const size_t k = first + i, slot = cl * kMaxClusterSize + i;
+                        const DTri& t = tris[C.order[k]];
+                        s0[slot] = float4_t{t.ax, t.ay, t.az, t.abx};
+                        s1[slot] = float4_t{t.aby, t.abz, t.acx, t.acy};
+                        float rk;
+                        std::memcpy(&rk, &C.rank[k], 4);
+                        s2[slot] = float4_t{t.acz, rk, 0.f, 0.f};
+                        sf[slot] = t.face;
+                        uint32_t packed = 0;
+                        for (int a = 0; a < 3; ++a) {
+                            long v = std::lround(double(C.normal[3 * k + a]) / double(q));
+                            v = std::max(-511L, std::min(511L, v));
+                            packed |= (uint32_t(v) & 1023u) << (10 * a);
+                        }
+                        nw[slot] = packed;
+                    }
                 }
                 if (C.rec.empty()) C.rec.assign(8, 0.f);
                 if ((rc = dev_upload(c, C.rec.data(), C.rec.size() * sizeof(float), &p))) return rc;
                 dm.clus = static_cast<const float4_t*>(p);
                 if ((rc = dev_upload(c, C.range.data(), C.range.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cl_range = static_cast<const uint32_t*>(p);
+                if ((rc = dev_upload(c, nw.data(), nw.size() * sizeof(uint32_t), &p))) return rc;
+                dm.cnrm = static_cast<const uint4_t*>(p);
                 if ((rc = dev_upload(c, s0.data(), s0.size() * sizeof(float4_t), &p))) return rc;
                 dm.c0 = static_cast<const float4_t*>(p);
                 if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
@@ -662,8 +702,6 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 dm.c2 = static_cast<const float4_t*>(p);
                 if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cface = static_cast<const uint32_t*>(p);
-                if ((rc = dev_upload(c, sr.data(), sr.size() * sizeof(uint32_t), &p))) return rc;
-                dm.crank = static_cast<const uint32_t*>(p);
                 c->nclusters += int64_t(C.rec.size() / 8);
             }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
@@ -828,7 +866,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.error_flag = c->d_error;
     P.counters = nullptr;
     P.xcd_chunk = xcd_chunk();
-    const int wave = sched_of(variant);
+    const int wave = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(launch_render(c, P, wave, s));
     HIPCHK(hipEventRecord(c->ev_stop, s));
@@ -899,7 +937,7 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.framebuffer = static_cast<uint32_t*>(fb);
     P.error_flag = c->d_error;
     P.counters = static_cast<unsigned long long*>(ctr);
-    const int sc = sched_of(variant);
+    const int sc = auto_sched(variant, *cam);
     HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
     unsigned long long h[10];

@@ -13,8 +13,9 @@
 //   * D depends on det, which is not known per cluster: the box is grown twice, for det >= kTol
 //     (loose) and det >= kTau (tight). Missing the loose box skips the cluster. Inside the
 //     tight box every front-facing primitive is a candidate. In between, only primitives whose
-//     det could lie in [kTol, kTau) are: the det estimate -(d . n) (n = ab x ac, one 16-B
-//     load) is within 16 eps |ab||ac| of the computed det, which sets the screen's margins.
+//     det could lie in [kTol, kTau) are: the det estimate -(d . n) (n = ab x ac, stored per
+//     cluster as 10-bit multiples of one step) is within a bounded margin of the computed det
+//     (cluster_step), which widens the screen's band.
 //     Back-facing primitives (det < kTol) are screened out the same way in both cases.
 //   * inside the leaf the reference keeps the FIRST primitive (leaf order) with the smallest t
 //     below the incoming best (strict <, kd_tree.cpp:440-456); clusters change the visiting
@@ -40,14 +41,14 @@ struct LeafHit {
 };
 
 template <bool COUNT>
-__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, float acz, LeafHit& h,
+__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, LeafHit& h,
                                             Ctr& ct) {
     if constexpr (COUNT) ct.tri += 1;
-    const float4_t q0 = m.c0[k], q1 = m.c1[k];
+    const float4_t q0 = m.c0[k], q1 = m.c1[k], q2 = m.c2[k];
     float u = 0.f, v = 0.f;
-    const float dist = tri_hit(r, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, acz), u, v);
+    const float dist = tri_hit(r, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, q2.x), u, v);
     if (dist <= h.t && dist > kTol) {
-        const int32_t rk = int32_t(m.crank[k]);
+        const int32_t rk = __float_as_int(q2.y);
         if (dist < h.t || (h.rank >= 0 && rk < h.rank)) {
             h.t = dist;
             h.slot = k;
@@ -59,10 +60,10 @@ __device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint3
     }
 }
 
-// One cluster (record lo = {lo.xyz, P | (n - 1)}, hi = {hi.xyz, first slot}) of the current
+// Cluster c (record lo = {lo.xyz, P | (n - 1)}, hi = {hi.xyz, first slot}) of the current
 // leaf: padded box tests, then the screen and the full tests of its primitives.
 template <bool COUNT>
-__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, float4_t lo, float4_t hi, LeafHit& h,
+__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi, LeafHit& h,
                                              Ctr& ct) {
     const float ax = fabsf(r.inv.x), ay = fabsf(r.inv.y), az = fabsf(r.inv.z);
     const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
@@ -89,24 +90,35 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, floa
 #ifdef ATR_EXP_SKIP_LOOSE
     if (!tight) return;  // EXPERIMENT ONLY (not exact): cost of the loose-only screens
 #endif
-    const float mg = 16.0f * kEps * P;
-    const float dlo = kTol - mg, dhi = tight ? __builtin_inff() : kTau + mg;
-    const uint32_t first = __float_as_uint(hi.w);
-    const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u, last = first + n - 1;
+    // screen: det estimate -(d . n~) from the cluster's quantized normals (64 B, four loads in
+    // flight together). |n - n~| <= q/2 per component and every |n| component <= 511 q, so the
+    // estimate is within (|d.x| + |d.y| + |d.z|) 0.51 q + 16 eps 511 q of -(d . n), which is
+    // within 16 eps |ab||ac| of the computed det; the band is widened by the sum.
+    const float q = hi.w;
+    const float mq = (fabsf(r.d.x) + fabsf(r.d.y) + fabsf(r.d.z)) * (0.51f * q) + (16.0f * kEps * 511.0f) * q +
+                     16.0f * kEps * P;
+    const float dlo = kTol - mq, dhi = tight ? __builtin_inff() : kTau + mq;
+    const uint32_t first = kMaxClusterSize * c;
+    const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u;
     if constexpr (COUNT) ct.screen += n;
-    // screen four primitives per step (their normal loads in flight together)
-    for (uint32_t k = first; k <= last; k += 4) {
-        const uint32_t k1 = k + 1 <= last ? k + 1 : last, k2 = k + 2 <= last ? k + 2 : last,
-                       k3 = k + 3 <= last ? k + 3 : last;
-        const float4_t n0 = m.c2[k], n1 = m.c2[k1], n2 = m.c2[k2], n3 = m.c2[k3];
-        const float d0 = -(r.d.x * n0.x + r.d.y * n0.y + r.d.z * n0.z);
-        const float d1 = -(r.d.x * n1.x + r.d.y * n1.y + r.d.z * n1.z);
-        const float d2 = -(r.d.x * n2.x + r.d.y * n2.y + r.d.z * n2.z);
-        const float d3 = -(r.d.x * n3.x + r.d.y * n3.y + r.d.z * n3.z);
-        if (d0 >= dlo && d0 < dhi) cluster_tri<COUNT>(r, m, k, n0.w, h, ct);
-        if (k + 1 <= last && d1 >= dlo && d1 < dhi) cluster_tri<COUNT>(r, m, k + 1, n1.w, h, ct);
-        if (k + 2 <= last && d2 >= dlo && d2 < dhi) cluster_tri<COUNT>(r, m, k + 2, n2.w, h, ct);
-        if (k + 3 <= last && d3 >= dlo && d3 < dhi) cluster_tri<COUNT>(r, m, k + 3, n3.w, h, ct);
+    const uint4_t* nb = m.cnrm + 4 * size_t(c);
+    const float dx = r.d.x * q, dy = r.d.y * q, dz = r.d.z * q;  // d scaled once: e = -(d q . packed)
+    uint32_t cand = 0;
+    for (uint32_t g = 0; g < n; g += 4) {
+        const uint4_t w = nb[g / 4];
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float px = float(int32_t(ws[j] << 22) >> 22), py = float(int32_t(ws[j] << 12) >> 22),
+                        pz = float(int32_t(ws[j] << 2) >> 22);
+            const float e = -(dx * px + dy * py + dz * pz);
+            if (g + j < n && e >= dlo && e < dhi) cand |= 1u << (g + j);
+        }
+    }
+    while (cand) {  // full tests of the candidates, in slot order
+        const int k = __builtin_ctz(cand);
+        cand &= cand - 1;
+        cluster_tri<COUNT>(r, m, first + uint32_t(k), h, ct);
     }
 }
 

@@ -17,6 +17,7 @@
 namespace atr {
 
 struct alignas(16) float4_t { float x, y, z, w; };
+struct alignas(16) uint4_t { uint32_t x, y, z, w; };
 
 constexpr float kMaxFloat = 3.402823466e+38F;     // PL_base_defs.h:72
 constexpr float kInvU32Max = 2.328306437e-10F;    // PL_base_defs.h:75
@@ -24,6 +25,7 @@ constexpr float kTol = 0.0001f;                   // ray.h:5
 constexpr int kMaskLevels = 16;                   // traversal mask-stack depth (8 bits/level)
 constexpr int kMaxMaterials = 32;
 constexpr int kMaxModels = 8;
+constexpr int kMaxClusterSize = 16;  // primitive slots per leaf cluster (ATR_CLUSTER_SIZE <= this)
 
 struct V3 { float x, y, z; };
 ATR_HD V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -104,16 +106,17 @@ struct DModel {
     const float* t2;
     const uint32_t* tface;
     // leaf clusters, 2 float4 per cluster: {lo.xyz, bound of |ab||ac| with
-    // (n - 1) in its low 5 mantissa bits}, {hi.xyz, bits(first slot)}; cl_range = first
-    // cluster, count per node; the primitives again in cluster order: c0 = {a.xyz, ab.x},
-    // c1 = {ab.yz, ac.xy}, c2 = {n = ab x ac, ac.z}, their faces and leaf ranks
+    // (n - 1) in its low 5 mantissa bits}, {hi.xyz, q}; cl_range = first cluster, count per
+    // node. Cluster c owns the primitive slots [16 c, 16 c + n): cnrm = the normals n = ab x ac
+    // as 3 x 10-bit signed multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
+    // c1 = {ab.yz, ac.xy}, c2 = {ac.z, bits(leaf rank), 0, 0}, cface = face index
     const float4_t* clus;
     const uint32_t* cl_range;
+    const uint4_t* cnrm;
     const float4_t* c0;
     const float4_t* c1;
     const float4_t* c2;
     const uint32_t* cface;
-    const uint32_t* crank;
     const float* shade;          // 9 f32 per face: smooth -> na, nb, nc; flat -> v0, v1, v2
     uint32_t nfaces;
     int32_t has_tree;

@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256, kPersistOcc) void persist_kernel(RenderParams 
                 while (L.c < L.cend) {
                     const float4_t lo = nlo, hi = nhi;
                     if (L.c + 1 < L.cend) { nlo = m.clus[2 * L.c + 2]; nhi = m.clus[2 * L.c + 3]; }
-                    cluster_step<COUNT>(L.r, m, lo, hi, L.h, ct);
+                    cluster_step<COUNT>(L.r, m, L.c, lo, hi, L.h, ct);
                     ++L.c;
                 }
                 // stop at the first leaf that improved the hit (:457-460)

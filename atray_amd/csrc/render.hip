@@ -88,7 +88,7 @@ __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m
     for (uint32_t c = cfirst; c < cend; ++c) {
         const float4_t lo = nlo, hi = nhi;
         if (c + 1 < cend) { nlo = m.clus[2 * c + 2]; nhi = m.clus[2 * c + 3]; }
-        cluster_step<COUNT>(r, m, lo, hi, h, ct);
+        cluster_step<COUNT>(r, m, c, lo, hi, h, ct);
     }
     best_t = h.t;
     best_slot = h.slot;
