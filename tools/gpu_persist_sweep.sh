@@ -3,7 +3,7 @@
 # tools/build_exp.sh on c3 (primary) and c4-shaped multi-bounce (kprof, CLUSTER beside PERSIST).
 # Settings: SWEEP_NAME, SWEEP_LIBS, SWEEP_MB from the environment or build/sweep.env.
 [ -f build/sweep.env ] && . build/sweep.env
-EXP_NAME=${SWEEP_NAME:-sweep} EXP_VARIANTS=cl,ps EXP_LIBS="$SWEEP_LIBS" bash tools/gpu_exp.sh || exit 1
+EXP_NAME=${SWEEP_NAME:-sweep} EXP_VARIANTS=${SWEEP_VARIANTS:-cl,ps} EXP_PMC=$SWEEP_PMC EXP_LIBS="$SWEEP_LIBS" bash tools/gpu_exp.sh || exit 1
 if [ -n "$SWEEP_MB" ]; then
   mkdir -p gpurun_out/${SWEEP_NAME:-sweep}_mb
   for L in "" $SWEEP_LIBS; do
