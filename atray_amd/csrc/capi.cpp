@@ -102,6 +102,15 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     }
 }
 
+// IEEE binary16 bits of an integer |v| <= 2047 (exact).
+uint16_t half_of_int(int32_t v) {
+    if (v == 0) return 0;
+    const uint32_t sign = v < 0 ? 0x8000u : 0u;
+    uint32_t m = uint32_t(v < 0 ? -v : v);
+    int e = 31 - __builtin_clz(m);
+    return uint16_t(sign | (uint32_t(e + 15) << 10) | ((m << (10 - e)) & 0x3FFu));
+}
+
 int32_t env_int(const char* name, int32_t dflt) {
     const char* e = std::getenv(name);
     return e ? std::atoi(e) : dflt;
@@ -653,7 +662,9 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 std::vector<float4_t> s0(ns, float4_t{0.f, 0.f, 0.f, 0.f}), s1(ns, float4_t{0.f, 0.f, 0.f, 0.f});
                 std::vector<float4_t> s2(ns, float4_t{0.f, 0.f, 0.f, 0.f});
                 std::vector<uint32_t> sf(ns, 0u);
-                std::vector<uint32_t> nw(ns, 0u);  // 16 packed normals per cluster
+                // screen normals, 24 u32 per cluster: (nx, ny) of slot k as f16 in word k, then
+                // (nz of slot 2i, nz of slot 2i + 1) in word 16 + i (cluster.h)
+                std::vector<uint32_t> nw(std::max<size_t>(1, ncl) * 24, 0u);
                 for (size_t cl = 0; cl < ncl; ++cl) {
                     uint32_t pw, first;
                     std::memcpy(&pw, &C.rec[8 * cl + 3], 4);
@@ -661,7 +672,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                     const uint32_t n = (pw & 31u) + 1u;
                     if (n > uint32_t(kMaxClusterSize)) return ATR_E_INVALID;
                     // screen normals: a step q >= max |n component| / 511 and each normal as
-                    // round(n / q) in 3 x 10 bits (|n - q * packed| <= q / 2 per component)
+                    // round(n / q), integers of at most 511 (exact in f16; |n - q p| <= q / 2)
                     double mx = 0.0;
                     for (uint32_t k = first; k < first + n; ++k)
                         for (int a = 0; a < 3; ++a) mx = std::max(mx, std::fabs(double(C.normal[3 * k + a])));
@@ -678,13 +689,14 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                         std::memcpy(&rk, &C.rank[k], 4);
                         s2[slot] = float4_t{t.acz, rk, 0.f, 0.f};
                         sf[slot] = t.face;
-                        uint32_t packed = 0;
+                        uint16_t h[3];
                         for (int a = 0; a < 3; ++a) {
                             long v = std::lround(double(C.normal[3 * k + a]) / double(q));
                             v = std::max(-511L, std::min(511L, v));
-                            packed |= (uint32_t(v) & 1023u) << (10 * a);
+                            h[a] = half_of_int(int32_t(v));
                         }
-                        nw[slot] = packed;
+                        nw[24 * cl + i] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
+                        nw[24 * cl + 16 + i / 2] |= uint32_t(h[2]) << (16 * (i & 1));
                     }
                 }
                 if (C.rec.empty()) C.rec.assign(8, 0.f);

@@ -14,7 +14,7 @@
 //     (loose) and det >= kTau (tight). Missing the loose box skips the cluster. Inside the
 //     tight box every front-facing primitive is a candidate. In between, only primitives whose
 //     det could lie in [kTol, kTau) are: the det estimate -(d . n) (n = ab x ac, stored per
-//     cluster as 10-bit multiples of one step) is within a bounded margin of the computed det
+//     cluster as f16 integer multiples of one step) is within a bounded margin of the computed det
 //     (cluster_step), which widens the screen's band.
 //     Back-facing primitives (det < kTol) are screened out the same way in both cases.
 //   * inside the leaf the reference keeps the FIRST primitive (leaf order) with the smallest t
@@ -90,28 +90,36 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
 #ifdef ATR_EXP_SKIP_LOOSE
     if (!tight) return;  // EXPERIMENT ONLY (not exact): cost of the loose-only screens
 #endif
-    // screen: det estimate -(d . n~) from the cluster's quantized normals (64 B, four loads in
-    // flight together). |n - n~| <= q/2 per component and every |n| component <= 511 q, so the
-    // estimate is within (|d.x| + |d.y| + |d.z|) 0.51 q + 16 eps 511 q of -(d . n), which is
-    // within 16 eps |ab||ac| of the computed det; the band is widened by the sum.
+    // screen: det estimate -q (d . p) with the cluster's quantized normals n ~ q p (p integers
+    // of at most 511, f16, 96 B per cluster) and d rounded to f16, two f16 dot products per
+    // primitive. |n - q p| <= q/2 per component, d's f16 rounding <= 2^-11 |d_a| + 2^-25, the
+    // f32 accumulation a few eps: the estimate is within
+    //   (|d.x| + |d.y| + |d.z|) q (0.51 + 511 (2^-11 + 8 eps)) + 16 eps 511 q + 2^-20 q
+    // of -(d . n), which is within 16 eps |ab||ac| of the computed det; the band is widened by it.
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const float q = hi.w;
-    const float mq = (fabsf(r.d.x) + fabsf(r.d.y) + fabsf(r.d.z)) * (0.51f * q) + (16.0f * kEps * 511.0f) * q +
-                     16.0f * kEps * P;
+    const float sd = fabsf(r.d.x) + fabsf(r.d.y) + fabsf(r.d.z);
+    const float mq = sd * (q * (0.51f + 511.0f * (4.8828125e-4f + 8.0f * kEps))) +
+                     q * (16.0f * kEps * 511.0f + 9.5367432e-7f) + 16.0f * kEps * P;
     const float dlo = kTol - mq, dhi = tight ? __builtin_inff() : kTau + mq;
     const uint32_t first = kMaxClusterSize * c;
     const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u;
     if constexpr (COUNT) ct.screen += n;
-    const uint4_t* nb = m.cnrm + 4 * size_t(c);
-    const float dx = r.d.x * q, dy = r.d.y * q, dz = r.d.z * q;  // d scaled once: e = -(d q . packed)
+    const h2 dxy = {(_Float16)r.d.x, (_Float16)r.d.y};
+    const _Float16 hz = (_Float16)r.d.z;
+    const h2 dz_lo = {hz, (_Float16)0.0f}, dz_hi = {(_Float16)0.0f, hz};
+    const uint4_t* nb = m.cnrm + 6 * size_t(c);
+    const float nq = -q;
     uint32_t cand = 0;
-    for (uint32_t g = 0; g < n; g += 4) {
-        const uint4_t w = nb[g / 4];
-        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    for (uint32_t g = 0; g < n; g += 8) {  // eight primitives per step: (nx, ny) x 8, nz x 8
+        const uint4_t a0 = nb[g / 4], a1 = nb[g / 4 + 1], z = nb[4 + g / 8];
+        const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float px = float(int32_t(ws[j] << 22) >> 22), py = float(int32_t(ws[j] << 12) >> 22),
-                        pz = float(int32_t(ws[j] << 2) >> 22);
-            const float e = -(dx * px + dy * py + dz * pz);
+        for (int j = 0; j < 8; ++j) {
+            const h2 pxy = __builtin_bit_cast(h2, xy[j]), pz = __builtin_bit_cast(h2, zz[j / 2]);
+            const float dz = __builtin_amdgcn_fdot2((j & 1) ? dz_hi : dz_lo, pz, 0.0f, false);
+            const float e = __builtin_amdgcn_fdot2(dxy, pxy, dz, false) * nq;
             if (g + j < n && e >= dlo && e < dhi) cand |= 1u << (g + j);
         }
     }

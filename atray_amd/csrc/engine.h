@@ -107,8 +107,8 @@ struct DModel {
     const uint32_t* tface;
     // leaf clusters, 2 float4 per cluster: {lo.xyz, bound of |ab||ac| with
     // (n - 1) in its low 5 mantissa bits}, {hi.xyz, q}; cl_range = first cluster, count per
-    // node. Cluster c owns the primitive slots [16 c, 16 c + n): cnrm = the normals n = ab x ac
-    // as 3 x 10-bit signed multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
+    // node. Cluster c owns the primitive slots [16 c, 16 c + n): cnrm = 6 uint4 of its normals
+    // n = ab x ac as f16 integer multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
     // c1 = {ab.yz, ac.xy}, c2 = {ac.z, bits(leaf rank), 0, 0}, cface = face index
     const float4_t* clus;
     const uint32_t* cl_range;
