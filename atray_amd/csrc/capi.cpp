@@ -8,6 +8,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fcntl.h>
+#include <unistd.h>
+#include <cerrno>
 #include <mutex>
 #include <new>
 #include <string>
@@ -54,10 +57,12 @@ struct BlockSet {
     int64_t packed_pixels = 0;
 };
 
+// first_emit > 0: the pixels of tiles[0, first_emit) are left out (they belong to an earlier
+// launch of a progressive render) and only tiles[first_emit, ntiles) emit blocks.
 void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, std::vector<DBlock>& out,
-                  int64_t& npix) {
+                  int64_t& npix, int32_t first_emit = 0) {
     const int32_t cw = (W + 7) / 8, ch = (H + 7) / 8;
-    std::vector<uint64_t> cell(size_t(cw) * size_t(ch), 0);
+    std::vector<uint64_t> cell(size_t(cw) * size_t(ch), 0), done(first_emit > 0 ? cell.size() : 0, 0);
     // tile order decides the block order: cells are emitted tile by tile (first owner wins)
     std::vector<int32_t> order;
     order.reserve(cell.size());
@@ -81,6 +86,8 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
                         if (x >= t.min_x && x <= t.max_x) m |= uint64_t(1) << (ly * 8 + lx);
                     }
                 }
+                if (k < first_emit) { done[ci] |= m; continue; }
+                if (first_emit > 0) m &= ~done[ci];
                 if (!m) continue;
                 if (!seen[ci]) { seen[ci] = 1; order.push_back(int32_t(ci)); }
                 cell[ci] |= m;
@@ -163,6 +170,12 @@ struct atr_ctx {
     hipEvent_t qev[kQueueSlots] = {};
     bool qused[kQueueSlots] = {};
     int qnext = 0;
+    // progressive render (atr_render_start_progressive): one launch per tile group, an event
+    // after each; prog_end[g] = tiles complete once group g is
+    bool prog_active = false;
+    std::vector<DevBuf> prog_blocks;
+    std::vector<hipEvent_t> prog_ev;
+    std::vector<int32_t> prog_end;
 };
 
 namespace {
@@ -476,6 +489,62 @@ int atr_camera_set(atr_camera* cm, atr_vec3 eye, atr_vec3 facing, int32_t w, int
     return ATR_OK;
 }
 
+namespace {
+void put_le(uint8_t* p, uint32_t v, int n) {
+    for (int i = 0; i < n; ++i) p[i] = uint8_t(v >> (8 * i));
+}
+}  // namespace
+
+int atr_write_bmp(const uint32_t* pixels, int32_t width, int32_t height, const char* name, char* out_path,
+                  int32_t out_cap) {
+    if (!pixels || !name || width <= 0 || height <= 0) return ATR_E_INVALID;
+    const size_t len = std::strlen(name);
+    if (len + 8 > 1024) return ATR_E_INVALID;  // the reference's new_name[1024]
+    const uint64_t bytes = uint64_t(width) * uint64_t(height) * 4;
+    if (bytes + 70 > 0x7FFFFFFFull) return ATR_E_INVALID;  // int32 total_file_size
+    uint8_t hdr[70] = {};
+    hdr[0] = 'B';
+    hdr[1] = 'M';
+    put_le(hdr + 2, uint32_t(70 + bytes), 4);  // total size; reserved1/2 = 0
+    put_le(hdr + 10, 70, 4);                   // pixel offset = 14 + 56
+    uint8_t* d = hdr + 14;
+    put_le(d + 0, 56, 4);
+    put_le(d + 4, uint32_t(width), 4);
+    put_le(d + 8, uint32_t(height), 4);  // positive: bottom-up rows, matching row 0 = bottom
+    put_le(d + 12, 1, 2);                // planes
+    put_le(d + 14, 32, 2);               // bits per pixel
+    put_le(d + 16, 3, 4);                // BI_BITFIELDS
+    put_le(d + 20, uint32_t(bytes), 4);
+    put_le(d + 24, 197, 4);  // ppm x, y as the reference sets them
+    put_le(d + 28, 39, 4);
+    put_le(d + 40, 0x00FF0000u, 4);  // clr_used/clr_important (32, 36) = 0; R, G, B, A masks
+    put_le(d + 44, 0x0000FF00u, 4);
+    put_le(d + 48, 0x000000FFu, 4);
+    put_le(d + 52, 0, 4);
+    std::string path;
+    int fd = -1;
+    for (uint32_t id = 0; id < 100 && fd < 0; ++id) {  // "%s_%u.bmp" fits len + 8 bytes for ids < 100
+        path = std::string(name) + "_" + std::to_string(id) + ".bmp";
+        fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0644);
+        if (fd < 0 && errno != EEXIST) return ATR_E_IO;
+    }
+    if (fd < 0) return ATR_E_IO;
+    bool ok = ::write(fd, hdr, sizeof(hdr)) == ssize_t(sizeof(hdr));
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(pixels);
+    for (uint64_t off = 0; ok && off < bytes;) {
+        const ssize_t w = ::write(fd, src + off, size_t(std::min<uint64_t>(bytes - off, 1ull << 30)));
+        ok = w > 0;
+        off += ok ? uint64_t(w) : 0;
+    }
+    ok = (::close(fd) == 0) && ok;
+    if (!ok) return ATR_E_IO;
+    if (out_path && out_cap > 0) {
+        std::strncpy(out_path, path.c_str(), size_t(out_cap) - 1);
+        out_path[out_cap - 1] = 0;
+    }
+    return ATR_OK;
+}
+
 int32_t atr_make_tiles(int32_t w, int32_t h, int32_t threads, atr_tile* out, int32_t cap) {
     return reference_tiles(w, h, threads, out, out ? cap : 0);
 }
@@ -528,6 +597,10 @@ int atr_destroy(atr_ctx* c) {
     if (c->wf_pinned) (void)hipHostFree(c->wf_pinned);
     if (c->d_error) (void)hipFree(c->d_error);
     if (c->qring) (void)hipFree(c->qring);
+    for (DevBuf& b : c->prog_blocks)
+        if (b.p) (void)hipFree(b.p);
+    for (hipEvent_t e : c->prog_ev)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->qev)
         if (e) (void)hipEventDestroy(e);
     (void)hipEventDestroy(c->ev_start);
@@ -832,6 +905,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     int rc = ATR_OK;
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
+    c->prog_active = false;
     if (variant == ATR_KERNEL_WAVEFRONT) {
         int64_t maxn = 1;
         for (int32_t v : c->model_nodes) maxn = std::max<int64_t>(maxn, v);
@@ -1014,6 +1088,70 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     return ATR_OK;
 }
 
+int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                                 const atr_frame* fr, uint64_t seed, void* stream, int32_t variant,
+                                 int32_t tiles_per_launch) {
+    if (!c || !cam || !fr || !fr->framebuffer || ntiles < 0 || (ntiles && !tiles) || tiles_per_launch < 1)
+        return ATR_E_INVALID;
+    if (cam->width <= 0 || cam->height <= 0 || cam->width > (1 << 16) || cam->height > (1 << 16)) return ATR_E_INVALID;
+    if (fr->layout != ATR_LAYOUT_IMAGE || variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (c->have_render) HIPCHK(hipEventSynchronize(c->ev_done));  // group buffers are reused
+    const int32_t ngroups = (ntiles + tiles_per_launch - 1) / tiles_per_launch;
+    while (int32_t(c->prog_ev.size()) < ngroups) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->prog_ev.push_back(e);
+    }
+    c->prog_blocks.resize(std::max<size_t>(c->prog_blocks.size(), size_t(ngroups)));
+    c->prog_end.assign(size_t(ngroups), 0);
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.layout = ATR_LAYOUT_IMAGE;
+    P.framebuffer = fr->framebuffer;
+    P.hit_face = fr->hit_face;
+    P.hit_t = fr->hit_t;
+    P.rgb = fr->rgb;
+    P.ray_casts = fr->ray_casts;
+    P.traced_rays = fr->traced_rays;
+    P.error_flag = c->d_error;
+    P.xcd_chunk = xcd_chunk();
+    const int sched = auto_sched(variant, *cam);
+    HIPCHK(hipEventRecord(c->ev_start, s));
+    for (int32_t g = 0; g < ngroups; ++g) {
+        const int32_t a = g * tiles_per_launch, e = std::min(ntiles, a + tiles_per_launch);
+        std::vector<DBlock> blocks;
+        int64_t npix = 0;
+        build_blocks(tiles, e, cam->width, cam->height, blocks, npix, a);  // tiles[a, e), new pixels
+        DevBuf& d = c->prog_blocks[size_t(g)];
+        const size_t need = std::max<size_t>(blocks.size() * sizeof(DBlock), 32);
+        if (d.n < need) {
+            if (d.p) HIPCHK(hipFree(d.p));
+            d = DevBuf();
+            HIPCHK(hipMalloc(&d.p, need));
+            d.n = need;
+        }
+        if (!blocks.empty()) HIPCHK(hipMemcpy(d.p, blocks.data(), blocks.size() * sizeof(DBlock), hipMemcpyHostToDevice));
+        P.blocks = static_cast<const DBlock*>(d.p);
+        P.nblocks = int32_t(blocks.size());
+        HIPCHK(launch_render(c, P, sched, s));
+        HIPCHK(hipEventRecord(c->prog_ev[size_t(g)], s));
+        c->prog_end[size_t(g)] = e;
+    }
+    HIPCHK(hipEventRecord(c->ev_stop, s));
+    HIPCHK(hipEventRecord(c->ev_done, s));
+    c->have_render = true;
+    c->prog_active = true;
+    c->last_stream = s;
+    c->last_ntiles = ntiles;
+    return ATR_OK;
+}
+
 int atr_render_start(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                      const atr_frame* fr, uint64_t seed, void* stream) {
     return atr_render_start_ex(c, cam, tiles, ntiles, fr, seed, stream, ATR_KERNEL_AUTO);
@@ -1030,7 +1168,16 @@ int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) return -(1000 + int(q));
         const auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
-        if (uint32_t(el.count()) >= timeout_ms) return 1;
+        if (uint32_t(el.count()) >= timeout_ms) {
+            if (tiles_done && c->prog_active) {  // tiles of the leading groups already complete
+                for (size_t g = 0; g < c->prog_end.size(); ++g) {
+                    const hipError_t qg = hipEventQuery(c->prog_ev[g]);
+                    if (qg != hipSuccess) break;
+                    *tiles_done = c->prog_end[g];
+                }
+            }
+            return 1;
+        }
         std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
     int32_t err = 0;

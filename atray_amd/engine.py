@@ -92,7 +92,7 @@ EXPORTS = [
     "atr_render_counters", "atr_render_tile_costs", "atr_render_wave_trace", "atr_balance_shard_tiles",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
-    "atr_memset_d",
+    "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp",
 ]
 
 _lib = None
@@ -141,6 +141,9 @@ def lib():
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
+        "atr_render_start_progressive": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32, i32],
+                                         C.c_int),
+        "atr_write_bmp": ([vp, i32, i32, C.c_char_p, C.c_char_p, i32], C.c_int),
         "atr_last_kernel_ms": ([vp, P(C.c_float)], C.c_int),
         "atr_device_alloc": ([vp, C.c_size_t, P(vp)], C.c_int),
         "atr_device_free": ([vp, vp], C.c_int),
@@ -213,6 +216,17 @@ def make_shard_tiles(width, height, side, rank, world):
     buf = (atr_tile * max(1, n))()
     L.atr_make_shard_tiles(width, height, side, rank, world, C.cast(buf, C.c_void_p), n)
     return np.array([[t.min_x, t.min_y, t.max_x, t.max_y] for t in buf[:n]], np.int32).reshape(-1, 4)
+
+
+def write_bmp(pixels, name):
+    """BGRX (H, W) u32 image, row 0 = bottom -> '<name>_<id>.bmp' (texture.cpp:66-115); returns the path."""
+    px = np.ascontiguousarray(pixels, dtype=np.uint32)
+    if px.ndim != 2:
+        raise ValueError("write_bmp: pixels must be (height, width)")
+    out = C.create_string_buffer(len(os.fsencode(name)) + 32)
+    check(lib().atr_write_bmp(px.ctypes.data, px.shape[1], px.shape[0], os.fsencode(name), out, len(out)),
+          f"write bmp {name}")
+    return os.fsdecode(out.value)
 
 
 class Mesh:
@@ -358,6 +372,15 @@ class Engine:
                                         C.byref(frame), C.c_uint64(seed & (2**64 - 1)),
                                         C.c_void_p(stream) if stream else None, int(variant)),
               "render start")
+
+    def render_start_progressive(self, cam, tiles, frame: atr_frame, seed, tiles_per_launch, stream=None,
+                                 variant=ATR_KERNEL_AUTO):
+        """Live-view render: tiles_per_launch tiles per launch; wait() reports finished tiles."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_render_start_progressive(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n,
+                                                 C.byref(frame), C.c_uint64(seed & (2**64 - 1)),
+                                                 C.c_void_p(stream) if stream else None, int(variant),
+                                                 int(tiles_per_launch)), "progressive render start")
 
     def counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
         arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)

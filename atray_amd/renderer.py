@@ -135,7 +135,10 @@ class RenderInfo:
     _dev: dict = field(default_factory=dict)
 
 
-def start_render_from_camera(info: RenderInfo, engine: E.Engine) -> None:
+def start_render_from_camera(info: RenderInfo, engine: E.Engine, tiles_per_launch: int = 0) -> None:
+    """renderer.cpp:447-455. tiles_per_launch > 0 renders progressively for a live view
+    (app.cpp:162-186): wait_for_render_from_camera_to_finish then reports finished tiles in
+    jobs_done and refreshes camera_tex with them while the render runs."""
     import torch
     W, H = info.camera.render_settings.resolution
     tiles = E.make_tiles(W, H, info.threads)
@@ -146,19 +149,45 @@ def start_render_from_camera(info: RenderInfo, engine: E.Engine) -> None:
     casts = torch.zeros(H * W, dtype=torch.int32, device=dev)
     per_tile = torch.zeros(len(tiles), dtype=torch.int64, device=dev)
     frame = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, casts.data_ptr(), None)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    engine.render_start(info.camera.c, tiles, frame, info.seed, stream=stream)
-    info._dev = {"fb": fb, "casts": casts, "per_tile": per_tile, "tiles": tiles, "stream": stream}
+    d = {"fb": fb, "casts": casts, "per_tile": per_tile, "tiles": tiles}
+    if tiles_per_launch > 0:
+        # own stream, so the live copies (another stream) run beside the render
+        rs = torch.cuda.Stream(dev)
+        rs.wait_stream(torch.cuda.current_stream(dev))
+        d["render_stream"], d["copy_stream"] = rs, torch.cuda.Stream(dev)
+        d["host"] = torch.empty(H * W, dtype=torch.int32, pin_memory=True)
+        d["stream"] = rs.cuda_stream
+        engine.render_start_progressive(info.camera.c, tiles, frame, info.seed, tiles_per_launch, stream=rs.cuda_stream)
+    else:
+        d["stream"] = torch.cuda.current_stream(dev).cuda_stream
+        engine.render_start(info.camera.c, tiles, frame, info.seed, stream=d["stream"])
+    info._dev = d
+
+
+def _live_copy(info: RenderInfo) -> None:
+    import torch
+    d = info._dev
+    W, H = info.camera.render_settings.resolution
+    with torch.cuda.stream(d["copy_stream"]):
+        d["host"].copy_(d["fb"], non_blocking=True)
+    d["copy_stream"].synchronize()
+    info.camera_tex = d["host"].numpy().view(np.uint32).reshape(H, W).copy()
 
 
 def wait_for_render_from_camera_to_finish(info: RenderInfo, engine: E.Engine, ms_to_wait_for: int) -> bool:
     """TRUE while still rendering after the timeout, FALSE once done (renderer.cpp:457-471)."""
     rc, done = engine.wait(ms_to_wait_for)
-    if rc == 1:
-        return True
     d = info._dev
+    if rc == 1:
+        if "copy_stream" in d and done > info.jobs_done:
+            info.jobs_done = done
+            _live_copy(info)  # the pixels of the first `done` tiles are final
+        return True
     W, H = info.camera.render_settings.resolution
     engine.tile_ray_casts(d["tiles"], W, d["casts"].data_ptr(), d["per_tile"].data_ptr(), d["stream"])
+    if "render_stream" in d:
+        import torch
+        torch.cuda.current_stream(d["fb"].device).wait_stream(d["render_stream"])
     per_tile = d["per_tile"].cpu().numpy()
     for j, c in zip(info.jobs, per_tile.tolist()):
         j.ray_casts = int(c)
@@ -166,6 +195,13 @@ def wait_for_render_from_camera_to_finish(info: RenderInfo, engine: E.Engine, ms
     info.jobs_done = len(info.jobs)
     info.camera_tex = d["fb"].cpu().numpy().view(np.uint32).reshape(H, W)
     return False
+
+
+def write_to_file(info: RenderInfo, file_name: str) -> str:
+    """The app's 'save render' (texture.cpp:66-115 via app.cpp): camera_tex as <file_name>_<id>.bmp."""
+    if info.camera_tex is None:
+        raise ValueError("write_to_file: nothing rendered yet")
+    return E.write_bmp(info.camera_tex, file_name)
 
 
 def app_scene(obj_path: str, center=(0.0, -15.0, -38.0), use_tree=True, leaf=300) -> Scene:

@@ -118,6 +118,15 @@ int32_t atr_make_shard_tiles(int32_t width, int32_t height, int32_t side, int32_
 int32_t atr_balance_shard_tiles(int32_t width, int32_t height, int32_t side, int32_t world,
                                 const int64_t* costs, int64_t rank0_extra, int32_t* owner_out);
 
+/* Live-view output (texture.cpp:66-115, Write_To_File): the BGRX u32 image (row 0 = bottom) as a
+   32-bit BI_BITFIELDS BMP, 14-byte file header + 56-byte header, written to the first of
+   "<name>_0.bmp", "<name>_1.bmp", ... that does not exist yet (created exclusively). The path
+   taken goes to out_path (out_cap bytes, may be NULL). Like the reference's name buffer of
+   strlen(name) + 8 bytes, ids stop at 99: ATR_E_IO once <name>_0 .. <name>_99 all exist, or the
+   file cannot be created. Host memory only; no device needed. */
+int atr_write_bmp(const uint32_t* pixels, int32_t width, int32_t height, const char* name, char* out_path,
+                  int32_t out_cap);
+
 /* ---------------------------------------------------------------- device engine */
 typedef struct atr_ctx atr_ctx;
 int atr_create(int device, atr_ctx** out);
@@ -162,6 +171,13 @@ enum { ATR_KERNEL_AUTO = 0, ATR_KERNEL_LANE = 1, ATR_KERNEL_WAVE = 2, ATR_KERNEL
    immediately. */
 int atr_render_start(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                      const atr_frame* frame, uint64_t seed, void* stream);
+/* Progressive start for a live view (app.cpp:162-186): the tiles are rendered in list order,
+   tiles_per_launch per launch, so atr_render_wait's tiles_done grows while the render runs and
+   the finished tiles of the IMAGE framebuffer can be shown. Each pixel is still traced once (a
+   pixel of overlapping tiles belongs to the first), and every output equals atr_render_start's. */
+int atr_render_start_progressive(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                                 const atr_frame* frame, uint64_t seed, void* stream, int32_t variant,
+                                 int32_t tiles_per_launch);
 /* Like atr_render_start with an explicit kernel variant. */
 int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         const atr_frame* frame, uint64_t seed, void* stream, int32_t variant);

@@ -126,3 +126,37 @@ def test_packed_size_counts_union_of_overlapping_tiles():
     tiles = E.make_tiles(1280, 720, 8)  # inclusive tiles overlapping by one pixel
     assert E.packed_size(tiles) == 1280 * 720
     assert E.packed_size([[0, 0, 9, 9], [5, 5, 14, 14]]) == 100 + 100 - 25
+
+
+def test_write_bmp_layout_and_naming(tmp_path):
+    """texture.cpp:66-115: 14 + 56 byte headers, BI_BITFIELDS masks, the BGRX rows as stored
+    (row 0 = bottom, positive height), and the first free <name>_<id>.bmp."""
+    import struct
+    W, H = 5, 3
+    px = (np.arange(W * H, dtype=np.uint32) * 0x010203 + 0x00112233).reshape(H, W)
+    base = str(tmp_path / "render")
+    p0 = E.write_bmp(px, base)
+    p1 = E.write_bmp(px, base)
+    assert (p0, p1) == (base + "_0.bmp", base + "_1.bmp")
+    b = open(p0, "rb").read()
+    assert len(b) == 70 + W * H * 4
+    assert b[:2] == b"BM" and struct.unpack_from("<iHHI", b, 2) == (70 + W * H * 4, 0, 0, 70)
+    dib = struct.unpack_from("<IIIhhIIIIIIIIII", b, 14)
+    assert dib == (56, W, H, 1, 32, 3, W * H * 4, 197, 39, 0, 0, 0x00FF0000, 0x0000FF00, 0x000000FF, 0)
+    assert np.array_equal(np.frombuffer(b[70:], np.uint32).reshape(H, W), px)
+
+
+def test_write_bmp_id_limit_and_errors(tmp_path):
+    """The reference formats into strlen(name) + 8 bytes, so ids 0..99 fit; past them, and for
+    a path that cannot be created, the writer reports ATR_E_IO instead of writing nothing."""
+    px = np.zeros((1, 1), np.uint32)
+    base = str(tmp_path / "f")
+    for i in range(100):
+        open(f"{base}_{i}.bmp", "wb").close()
+    with pytest.raises(E.AtrError):
+        E.write_bmp(px, base)
+    with pytest.raises(E.AtrError):
+        E.write_bmp(px, str(tmp_path / "missing_dir" / "x"))
+    with pytest.raises(ValueError):
+        E.write_bmp(np.zeros(4, np.uint32), base)
+    assert E.lib().atr_write_bmp(None, 1, 1, b"x", None, 0) == -1  # ATR_E_INVALID

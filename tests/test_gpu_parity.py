@@ -41,7 +41,7 @@ def upload(eng, asset, tree=True, spheres=(), planes=(), materials=(SKY, MODEL))
     eng.upload(list(materials), [(m, t, box, 1)], spheres, planes)
 
 
-def run(eng, cam, tiles=None, layout=E.ATR_LAYOUT_IMAGE, variant=E.ATR_KERNEL_AUTO, seed=SEED):
+def run(eng, cam, tiles=None, layout=E.ATR_LAYOUT_IMAGE, variant=E.ATR_KERNEL_AUTO, seed=SEED, progressive=0):
     W, H = cam.width, cam.height
     if tiles is None:
         tiles = [[0, 0, W - 1, H - 1]]
@@ -55,9 +55,13 @@ def run(eng, cam, tiles=None, layout=E.ATR_LAYOUT_IMAGE, variant=E.ATR_KERNEL_AU
     traced = torch.zeros(1, dtype=torch.int64, device=dev)
     fr = E.atr_frame(layout, fb.data_ptr(), face.data_ptr(), t.data_ptr(), rgb.data_ptr(),
                      casts.data_ptr(), traced.data_ptr())
-    eng.render_start(cam, tiles, fr, seed, stream=torch.cuda.current_stream().cuda_stream, variant=variant)
-    rc, _ = eng.wait()
-    assert rc == 0
+    stream = torch.cuda.current_stream().cuda_stream
+    if progressive:
+        eng.render_start_progressive(cam, tiles, fr, seed, progressive, stream=stream, variant=variant)
+    else:
+        eng.render_start(cam, tiles, fr, seed, stream=stream, variant=variant)
+    rc, done = eng.wait()
+    assert rc == 0 and done == len(tiles)
     torch.cuda.synchronize()
     out = {"fb": fb.cpu().numpy().view(np.uint32), "face": face.cpu().numpy().view(np.uint32),
            "t": t.cpu().numpy(), "rgb": rgb.cpu().numpy().reshape(-1, 3),
@@ -163,6 +167,48 @@ def test_renderer_api_start_wait(eng):
     tiles = E.make_tiles(320, 180, 8)
     assert info.total_ray_casts == sum(int(gcasts[y0:y1 + 1, x0:x1 + 1].sum()) for x0, y0, x1, y1 in tiles)
     assert info.jobs_done == len(tiles) == 40
+
+
+def test_renderer_api_progressive_live_view(eng):
+    """Live view (app.cpp:162-186): tiles finish in groups while the render runs; every pixel
+    of a tile reported done is final, and the finished frame equals the one-shot render."""
+    from atray_amd import renderer as R
+    scene = R.app_scene(asset_path("Monkey"), center=CENTERS["Monkey"])
+    R.prep_scene(scene, eng)
+    rs = R.RenderSettings(resolution=(320, 180), samples_per_pixel=4, bounce_limit=5)
+    info = R.RenderInfo(camera=R.set_camera((0.1, 2.0, 0.0), (-0.1, -0.5, -1.0), rs, 1.0),
+                        scene=scene, seed=SEED)
+    _, gfb, gcasts = render("monkey_320x180_s4_b5")
+    tiles = E.make_tiles(320, 180, 8)
+    R.start_render_from_camera(info, eng, tiles_per_launch=3)
+    seen = []
+    while R.wait_for_render_from_camera_to_finish(info, eng, 0):
+        if not seen or info.jobs_done != seen[-1]:
+            seen.append(info.jobs_done)
+            for x0, y0, x1, y1 in tiles[:info.jobs_done]:
+                assert np.array_equal(info.camera_tex[y0:y1 + 1, x0:x1 + 1], gfb[y0:y1 + 1, x0:x1 + 1])
+    assert seen == sorted(seen) and all(v % 3 == 0 for v in seen)
+    assert np.array_equal(info.camera_tex, gfb) and info.jobs_done == 40
+    assert info.total_ray_casts == sum(int(gcasts[y0:y1 + 1, x0:x1 + 1].sum()) for x0, y0, x1, y1 in tiles)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_progressive_start_equals_one_shot(eng, variant):
+    """Tile groups with overlapping reference tiles: each pixel traced once (first tile owns it)."""
+    upload(eng, "Monkey", True)
+    W, H = 160, 90
+    tiles = E.make_tiles(W, H, 8)
+    cam = E.camera(W, H, 3, 4)
+    want = run(eng, cam, tiles=tiles, variant=variant)
+    if variant == E.ATR_KERNEL_WAVEFRONT:
+        with pytest.raises(E.AtrError):
+            run(eng, cam, tiles=tiles, variant=variant, progressive=7)
+        return
+    for per in (1, 7, 1000):
+        got = run(eng, cam, tiles=tiles, variant=variant, progressive=per)
+        for k in ("fb", "casts", "face", "rgb", "traced"):
+            assert np.array_equal(got[k], want[k]), (per, k)
+        assert np.array_equal(got["t"].view(np.uint32), want["t"].view(np.uint32))
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
