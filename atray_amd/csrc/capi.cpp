@@ -702,6 +702,28 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 range[2 * size_t(n) + 1] = T.children[size_t(n)] ? 0u : T.leaf_count[size_t(n)];
                 if (T.depth[size_t(n)] > c->max_depth) c->max_depth = T.depth[size_t(n)];
             }
+            // leaves are addressed by their static discovery rank on the device (inner_table)
+            std::vector<int32_t> leaf_rank;
+            {
+                std::vector<float4_t> inner;
+                if ((rc = inner_table(T, inner, leaf_rank))) return rc;
+                dm.ninner = int32_t(inner.size() / 3);
+                if (inner.empty()) inner.assign(3, float4_t{0.f, 0.f, 0.f, 0.f});
+                if ((rc = dev_upload(c, inner.data(), inner.size() * sizeof(float4_t), &p))) return rc;
+                dm.inner = static_cast<const float4_t*>(p);
+                if (dm.ninner > c->max_inner) c->max_inner = dm.ninner;
+            }
+            auto by_rank = [&](const std::vector<uint32_t>& per_node) {
+                std::vector<uint32_t> out(std::max<size_t>(2, per_node.size()), 0u);
+                for (int32_t n = 0; n < T.nnodes; ++n) {
+                    const int32_t k = leaf_rank[size_t(n)];
+                    if (k < 0) continue;
+                    out[2 * size_t(k)] = per_node[2 * size_t(n)];
+                    out[2 * size_t(k) + 1] = per_node[2 * size_t(n) + 1];
+                }
+                return out;
+            };
+            range = by_rank(range);
             std::vector<DTri> tris(T.prim_face.size());
             for (size_t k = 0; k < tris.size(); ++k) tris[k] = make_tri(&T.prim_vertices[9 * k], T.prim_face[k]);
             {
@@ -733,7 +755,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 const size_t ncl = C.rec.size() / 8;
                 const size_t ns = std::max<size_t>(1, ncl) * kMaxClusterSize;
                 std::vector<float4_t> s0(ns, float4_t{0.f, 0.f, 0.f, 0.f}), s1(ns, float4_t{0.f, 0.f, 0.f, 0.f});
-                std::vector<float4_t> s2(ns, float4_t{0.f, 0.f, 0.f, 0.f});
+                std::vector<c2_t> s2(ns, c2_t{});
                 std::vector<uint32_t> sf(ns, 0u);
                 // screen normals, 24 u32 per cluster: (nx, ny) of slot k as f16 in word k, then
                 // (nz of slot 2i, nz of slot 2i + 1) in word 16 + i (cluster.h)
@@ -760,7 +782,8 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                         s1[slot] = float4_t{t.aby, t.abz, t.acx, t.acy};
                         float rk;
                         std::memcpy(&rk, &C.rank[k], 4);
-                        s2[slot] = float4_t{t.acz, rk, 0.f, 0.f};
+                        s2[slot].x = t.acz;
+                        s2[slot].y = rk;
                         sf[slot] = t.face;
                         uint16_t h[3];
                         for (int a = 0; a < 3; ++a) {
@@ -775,6 +798,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 if (C.rec.empty()) C.rec.assign(8, 0.f);
                 if ((rc = dev_upload(c, C.rec.data(), C.rec.size() * sizeof(float), &p))) return rc;
                 dm.clus = static_cast<const float4_t*>(p);
+                C.range = by_rank(C.range);
                 if ((rc = dev_upload(c, C.range.data(), C.range.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cl_range = static_cast<const uint32_t*>(p);
                 if ((rc = dev_upload(c, nw.data(), nw.size() * sizeof(uint32_t), &p))) return rc;
@@ -783,23 +807,14 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 dm.c0 = static_cast<const float4_t*>(p);
                 if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
                 dm.c1 = static_cast<const float4_t*>(p);
-                if ((rc = dev_upload(c, s2.data(), s2.size() * sizeof(float4_t), &p))) return rc;
-                dm.c2 = static_cast<const float4_t*>(p);
+                if ((rc = dev_upload(c, s2.data(), s2.size() * sizeof(c2_t), &p))) return rc;
+                dm.c2 = static_cast<const c2_t*>(p);
                 if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cface = static_cast<const uint32_t*>(p);
                 c->nclusters += int64_t(C.rec.size() / 8);
             }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
             dm.nodes = static_cast<const DNode*>(p);
-            {
-                std::vector<float4_t> inner;
-                if ((rc = inner_table(T, inner))) return rc;
-                dm.ninner = int32_t(inner.size() / 3);
-                if (inner.empty()) inner.assign(3, float4_t{0.f, 0.f, 0.f, 0.f});
-                if ((rc = dev_upload(c, inner.data(), inner.size() * sizeof(float4_t), &p))) return rc;
-                dm.inner = static_cast<const float4_t*>(p);
-                if (dm.ninner > c->max_inner) c->max_inner = dm.ninner;
-            }
             if ((rc = dev_upload(c, range.data(), range.size() * sizeof(uint32_t), &p))) return rc;
             dm.leaf_range = static_cast<const uint32_t*>(p);
             if ((rc = dev_upload(c, tris.data(), tris.size() * sizeof(DTri), &p))) return rc;

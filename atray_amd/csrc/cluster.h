@@ -41,10 +41,9 @@ struct LeafHit {
 };
 
 template <bool COUNT>
-__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, LeafHit& h,
-                                            Ctr& ct) {
+__device__ __forceinline__ void cluster_tri_test(const Ray& r, float4_t q0, float4_t q1, c2_t q2, uint32_t k,
+                                                 LeafHit& h, Ctr& ct) {
     if constexpr (COUNT) ct.tri += 1;
-    const float4_t q0 = m.c0[k], q1 = m.c1[k], q2 = m.c2[k];
     float u = 0.f, v = 0.f;
     const float dist = tri_hit(r, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, q2.x), u, v);
     if (dist <= h.t && dist > kTol) {
@@ -60,11 +59,17 @@ __device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint3
     }
 }
 
+template <bool COUNT>
+__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, LeafHit& h,
+                                            Ctr& ct) {
+    cluster_tri_test<COUNT>(r, m.c0[k], m.c1[k], m.c2[k], k, h, ct);
+}
+
 // Cluster c (record lo = {lo.xyz, P | (n - 1)}, hi = {hi.xyz, first slot}) of the current
 // leaf: padded box tests, then the screen and the full tests of its primitives.
 template <bool COUNT>
-__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi, LeafHit& h,
-                                             Ctr& ct) {
+__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
+                                             const uint4_t* pre, LeafHit& h, Ctr& ct) {
     const float ax = fabsf(r.inv.x), ay = fabsf(r.inv.y), az = fabsf(r.inv.z);
     const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
     const float fx = fmaxf(fabsf(lo.x - r.o.x), fabsf(hi.x - r.o.x));
@@ -112,7 +117,8 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     const float nq = -q;
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8) {  // eight primitives per step: (nx, ny) x 8, nz x 8
-        const uint4_t a0 = nb[g / 4], a1 = nb[g / 4 + 1], z = nb[4 + g / 8];
+        const uint4_t a0 = (pre && g == 0) ? pre[0] : nb[g / 4], a1 = (pre && g == 0) ? pre[1] : nb[g / 4 + 1],
+                      z = (pre && g == 0) ? pre[2] : nb[4 + g / 8];
         const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
 #pragma unroll
@@ -123,10 +129,57 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
             if (g + j < n && e >= dlo && e < dhi) cand |= 1u << (g + j);
         }
     }
-    while (cand) {  // full tests of the candidates, in slot order
-        const int k = __builtin_ctz(cand);
+#ifdef ATR_EXP_NO_TRI
+    if (cand) h.improved |= (cand == 0x12345u);  // EXPERIMENT ONLY (not exact): no full tests
+    cand = 0;
+#endif
+    while (cand) {  // full tests of the candidates in slot order, two primitives' loads in flight
+        const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
         cand &= cand - 1;
-        cluster_tri<COUNT>(r, m, first + uint32_t(k), h, ct);
+        const float4_t a0 = m.c0[ka], a1 = m.c1[ka];
+        const c2_t a2 = m.c2[ka];
+        if (cand) {
+            const uint32_t kb = first + uint32_t(__builtin_ctz(cand));
+            cand &= cand - 1;
+            const float4_t b0 = m.c0[kb], b1 = m.c1[kb];
+            const c2_t b2 = m.c2[kb];
+            cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
+            cluster_tri_test<COUNT>(r, b0, b1, b2, kb, h, ct);
+        } else {
+            cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
+        }
+    }
+}
+
+// Clusters [c, cend) of one leaf, the next cluster's record (and, with ATR_NRM_PREFETCH, its
+// first eight screen normals) in flight while the current one is screened.
+template <bool COUNT>
+__device__ __forceinline__ void cluster_range(const Ray& r, const DModel& m, uint32_t c, uint32_t cend, LeafHit& h,
+                                              Ctr& ct) {
+    if (c >= cend) return;
+    float4_t nlo = m.clus[2 * c], nhi = m.clus[2 * c + 1];
+#ifdef ATR_NRM_PREFETCH
+    uint4_t np[3] = {m.cnrm[6 * size_t(c)], m.cnrm[6 * size_t(c) + 1], m.cnrm[6 * size_t(c) + 4]};
+#endif
+    for (; c < cend; ++c) {
+        const float4_t lo = nlo, hi = nhi;
+#ifdef ATR_NRM_PREFETCH
+        const uint4_t cp[3] = {np[0], np[1], np[2]};
+#endif
+        if (c + 1 < cend) {
+            nlo = m.clus[2 * c + 2];
+            nhi = m.clus[2 * c + 3];
+#ifdef ATR_NRM_PREFETCH
+            np[0] = m.cnrm[6 * size_t(c + 1)];
+            np[1] = m.cnrm[6 * size_t(c + 1) + 1];
+            np[2] = m.cnrm[6 * size_t(c + 1) + 4];
+#endif
+        }
+#ifdef ATR_NRM_PREFETCH
+        cluster_step<COUNT>(r, m, c, lo, hi, cp, h, ct);
+#else
+        cluster_step<COUNT>(r, m, c, lo, hi, nullptr, h, ct);
+#endif
     }
 }
 

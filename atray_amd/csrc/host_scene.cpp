@@ -361,12 +361,40 @@ int atr::leaf_clusters(const HostTree& T, int size, LeafClusters& C) {
     return ATR_OK;
 }
 
-int atr::inner_table(const HostTree& T, std::vector<float4_t>& out) {
+int atr::inner_table(const HostTree& T, std::vector<float4_t>& out, std::vector<int32_t>& leaf_rank) {
     const int32_t n = T.nnodes;
     std::vector<int32_t> rank(size_t(n), -1);
     int32_t ninner = 0;
     for (int32_t i = 0; i < n; ++i)
         if (T.children[size_t(i)]) rank[size_t(i)] = ninner++;
+    // Static discovery order of the leaves: the traversal examines all children of a node (leaf
+    // children found in child order) before descending, and descends into the inner children
+    // highest first, each subtree completely before the next (the LIFO hit stack,
+    // kd_tree.cpp:363-435). Any single pass discovers its leaves in this order restricted to the
+    // ones it reaches, so the rank replaces the per-pass discovery index as the tie key.
+    leaf_rank.assign(size_t(n), -1);
+    if (n > 0) {
+        int32_t next = 0;
+        std::vector<int32_t> stack{0};
+        if (T.children[0] == 0) leaf_rank[0] = next++;
+        while (!stack.empty()) {
+            const int32_t x = stack.back();
+            stack.pop_back();
+            const int32_t c = T.children[size_t(x)];
+            if (!c) continue;
+            if (c < 0 || c + 8 > n) return ATR_E_INVALID;
+            for (int k = 0; k < 8; ++k)
+                if (T.children[size_t(c + k)] == 0) {
+                    if (leaf_rank[size_t(c + k)] >= 0) return ATR_E_INVALID;  // shared child: not a tree
+                    leaf_rank[size_t(c + k)] = next++;
+                }
+            for (int k = 0; k < 8; ++k)
+                if (T.children[size_t(c + k)]) {
+                    if (int32_t(stack.size()) > n) return ATR_E_INVALID;
+                    stack.push_back(c + k);
+                }
+        }
+    }
     out.assign(3 * size_t(ninner), float4_t{0.f, 0.f, 0.f, 0.f});
     auto same = [](float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; };
     for (int32_t i = 0; i < n; ++i) {
@@ -378,7 +406,7 @@ int atr::inner_table(const HostTree& T, std::vector<float4_t>& out) {
         const float lo[3] = {b[0], b[1], b[2]}, hi[3] = {b[3], b[4], b[5]};
         const float v[3] = {b0[3], b0[4], b0[5]};  // bb_left.aabb.max = division point
         uint32_t leafm = 0;
-        int32_t base = -1;
+        int32_t base = -1, leaf0 = -1;
         for (int k = 0; k < 8; ++k) {
             const float* cb = &T.bounds[6 * size_t(c + k)];
             const int bit[3] = {k >> 2, (k >> 1) & 1, k & 1};  // x: left/right, y: bottom/top, z: back/front
@@ -386,14 +414,20 @@ int atr::inner_table(const HostTree& T, std::vector<float4_t>& out) {
                 const float mn = bit[a] ? v[a] : lo[a], mx = bit[a] ? hi[a] : v[a];
                 if (!same(cb[a], mn) || !same(cb[3 + a], mx)) return ATR_E_TREE_LAYOUT;
             }
-            if (T.children[size_t(c + k)] == 0) leafm |= 1u << k;
-            else if (base < 0) base = rank[size_t(c + k)];
+            if (T.children[size_t(c + k)] == 0) {
+                leafm |= 1u << k;
+                if (leaf0 < 0) leaf0 = leaf_rank[size_t(c + k)];
+                if (leaf_rank[size_t(c + k)] != leaf0 + __builtin_popcount(leafm) - 1) return ATR_E_INVALID;
+            } else if (base < 0) {
+                base = rank[size_t(c + k)];
+            }
         }
         if (base < 0) base = 0;
+        if (leaf0 < 0) leaf0 = 0;
         const int32_t par = T.parent.empty() || T.parent[size_t(i)] < 0 ? -1 : rank[size_t(T.parent[size_t(i)])];
         const uint32_t bm = (uint32_t(base) << 8) | leafm;
         float w[3];
-        std::memcpy(&w[0], &c, 4);
+        std::memcpy(&w[0], &leaf0, 4);
         std::memcpy(&w[1], &par, 4);
         std::memcpy(&w[2], &bm, 4);
         float4_t* r = &out[3 * size_t(rank[size_t(i)])];

@@ -186,9 +186,9 @@ __device__ __forceinline__ void query_done(Lane<K>& L, const DModel& m, int32_t 
 // Head of the sorted leaf buffer becomes the leaf being scanned (kd_tree.cpp:437-441).
 template <int K, bool COUNT>
 __device__ __forceinline__ void begin_leaf(Lane<K>& L, const DModel& m, Ctr& ct) {
-    const int32_t leaf = L.lb.node[0];
+    const int32_t leaf = L.lb.leaf[0];
     L.bd = L.lb.d[0];
-    L.bi = L.lb.idx[0];
+    L.bi = L.lb.leaf[0];
     L.c = m.cl_range[2 * leaf];
     const uint32_t n = m.cl_range[2 * leaf + 1];
     L.cend = L.c + n;
@@ -309,14 +309,8 @@ __global__ __launch_bounds__(256, kPersistOcc) void persist_kernel(RenderParams 
         for (int32_t M = 0; M < nmodels; ++M) {
             const DModel& m = S->models[M];
             if (L.mi == M && L.ph == PH_SCAN) {  // the whole leaf (kd_tree.cpp:440-456)
-                float4_t nlo, nhi;  // next cluster's record, in flight while this one is screened
-                if (L.c < L.cend) { nlo = m.clus[2 * L.c]; nhi = m.clus[2 * L.c + 1]; }
-                while (L.c < L.cend) {
-                    const float4_t lo = nlo, hi = nhi;
-                    if (L.c + 1 < L.cend) { nlo = m.clus[2 * L.c + 2]; nhi = m.clus[2 * L.c + 3]; }
-                    cluster_step<COUNT>(L.r, m, L.c, lo, hi, L.h, ct);
-                    ++L.c;
-                }
+                cluster_range<COUNT>(L.r, m, L.c, L.cend, L.h, ct);
+                L.c = L.cend;
                 // stop at the first leaf that improved the hit (:457-460)
                 if (L.h.improved) {
                     query_done(L, m, M, nmodels);

@@ -82,14 +82,7 @@ __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m
     h.v = bv;
     h.rank = -1;
     h.improved = false;
-    const uint32_t cend = cfirst + ccount;
-    float4_t nlo, nhi;
-    if (ccount) { nlo = m.clus[2 * cfirst]; nhi = m.clus[2 * cfirst + 1]; }
-    for (uint32_t c = cfirst; c < cend; ++c) {
-        const float4_t lo = nlo, hi = nhi;
-        if (c + 1 < cend) { nlo = m.clus[2 * c + 2]; nhi = m.clus[2 * c + 3]; }
-        cluster_step<COUNT>(r, m, c, lo, hi, h, ct);
-    }
+    cluster_range<COUNT>(r, m, cfirst, cfirst + ccount, h, ct);
     best_t = h.t;
     best_slot = h.slot;
     bu = h.u;
@@ -98,7 +91,8 @@ __device__ __forceinline__ bool scan_leaf_clusters(const Ray& r, const DModel& m
 }
 
 template <bool COUNT, bool CL = false, int K = kLeafBuf>
-__device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m, Hit& h, int& err, Ctr& ct) {
+__device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m, const float4_t* __restrict__ tab, Hit& h,
+                                                  int& err, Ctr& ct) {
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
@@ -121,15 +115,15 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
         bool more = true;
         while (more) {
             LeafBuf<K> lb;
-            const int32_t n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+            const int32_t n = traverse_pass<K, COUNT>(r, tab, lb, bd, bi, ct);
             if (n < 0) { err = 1; break; }
             int32_t nb = n < K ? n : K;
             more = n > K;
             bool hit = false;
             while (nb > 0) {
-                const int32_t leaf = lb.node[0];
+                const int32_t leaf = lb.leaf[0];
                 bd = lb.d[0];
-                bi = lb.idx[0];
+                bi = lb.leaf[0];
                 if (scan(leaf)) { hit = true; break; }
                 lb_pop<K>(lb);
                 --nb;
@@ -162,10 +156,10 @@ __device__ __forceinline__ int32_t tq_next_leaf(TreeQuery& q, const Ray& r, cons
             q.state = 1;
         }
         const int32_t nb = q.ncand < kLeafBuf ? q.ncand : kLeafBuf;
-        if (q.pos < nb) return lb_node<kLeafBuf>(q.lb, q.pos);
+        if (q.pos < nb) return lb_leaf<kLeafBuf>(q.lb, q.pos);
         if (q.ncand <= kLeafBuf) { q.state = 2; return -1; }
         q.bd = q.lb.d[kLeafBuf - 1];
-        q.bi = q.lb.idx[kLeafBuf - 1];
+        q.bi = q.lb.leaf[kLeafBuf - 1];
         q.state = 0;
     }
 }
@@ -265,9 +259,9 @@ __device__ __forceinline__ int32_t tile_next_leaf(TreeQuery& q, const Ray& r, co
             if (q.ncand < 0) { err = 1; q.state = 2; return -1; }
             q.pos = q.ncand < kLeafBuf ? q.ncand : kLeafBuf;  // entries left in the buffer
             q.state = 1;
-            if (q.pos > 0) return q.lb.node[0];
+            if (q.pos > 0) return q.lb.leaf[0];
         }
-        if (q.pos > 0) return q.lb.node[0];
+        if (q.pos > 0) return q.lb.leaf[0];
         if (q.ncand <= kLeafBuf) { q.state = 2; return -1; }
         q.state = 0;
     }
@@ -366,7 +360,7 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
                 my_leaf = -1;
             } else {
                 q.bd = q.lb.d[0];
-                q.bi = q.lb.idx[0];
+                q.bi = q.lb.leaf[0];
                 lb_pop<kLeafBuf>(q.lb);
                 --q.pos;
                 my_leaf = tile_next_leaf<NW, COUNT>(q, r, m, err, ct);
@@ -398,14 +392,14 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
-                if (active) tree_closest_lane<COUNT, true>(r, m, h, err, ct);
+                if (active) tree_closest_lane<COUNT, true>(r, m, m.inner, h, err, ct);
                 else h.t = kMaxFloat;
             }
             else if constexpr (SCHED == SCHED_CLUSTER_K4) {  // 4-entry leaf buffer (fewer VGPRs)
-                if (active) tree_closest_lane<COUNT, true, 4>(r, m, h, err, ct);
+                if (active) tree_closest_lane<COUNT, true, 4>(r, m, m.inner, h, err, ct);
                 else h.t = kMaxFloat;
             }
-            else if (active) tree_closest_lane<COUNT>(r, m, h, err, ct);
+            else if (active) tree_closest_lane<COUNT>(r, m, m.inner, h, err, ct);
             else h.t = kMaxFloat;
             if (h.t > kTol && h.t < best) { best = h.t; face = h.face; fu = h.u; fv = h.v; nm = i; }
         } else if (active) {  // brute force (:58-82), face-ordered triangles, uniform loads

@@ -149,30 +149,27 @@ constexpr int kLeafBuf = 8;  // sorted leaves held per ray between DFS passes
 template <int K>
 struct LeafBuf {
     float d[K];
-    int32_t node[K];
-    int32_t idx[K];
+    int32_t leaf[K];  // leaf id = the leaf's rank in the static discovery order (inner_table)
 };
 
 template <int K>
 __device__ __forceinline__ void lb_clear(LeafBuf<K>& b) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) { b.d[j] = __builtin_inff(); b.node[j] = 0; b.idx[j] = 0; }
+    for (int j = 0; j < K; ++j) { b.d[j] = __builtin_inff(); b.leaf[j] = 0; }
 }
 
-// Insert a leaf discovered after every entry already held (larger discovery index): it goes
+// Insert a leaf discovered after every entry already held (larger discovery rank): it goes
 // behind every entry with distance <= dis, as the stable insertion sort does.
 template <int K>
-__device__ __forceinline__ void lb_insert(LeafBuf<K>& b, float dis, int32_t node, int32_t idx) {
+__device__ __forceinline__ void lb_insert(LeafBuf<K>& b, float dis, int32_t leaf) {
     if (!(dis < b.d[K - 1])) return;
     b.d[K - 1] = dis;
-    b.node[K - 1] = node;
-    b.idx[K - 1] = idx;
+    b.leaf[K - 1] = leaf;
 #pragma unroll
     for (int j = K - 1; j > 0; --j) {
         if (b.d[j] < b.d[j - 1]) {
             const float td = b.d[j]; b.d[j] = b.d[j - 1]; b.d[j - 1] = td;
-            const int32_t tn = b.node[j]; b.node[j] = b.node[j - 1]; b.node[j - 1] = tn;
-            const int32_t ti = b.idx[j]; b.idx[j] = b.idx[j - 1]; b.idx[j - 1] = ti;
+            const int32_t tl = b.leaf[j]; b.leaf[j] = b.leaf[j - 1]; b.leaf[j - 1] = tl;
         }
     }
 }
@@ -182,22 +179,22 @@ __device__ __forceinline__ void lb_insert(LeafBuf<K>& b, float dis, int32_t node
 template <int K>
 __device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
 #pragma unroll
-    for (int j = 0; j + 1 < K; ++j) { b.d[j] = b.d[j + 1]; b.node[j] = b.node[j + 1]; b.idx[j] = b.idx[j + 1]; }
+    for (int j = 0; j + 1 < K; ++j) { b.d[j] = b.d[j + 1]; b.leaf[j] = b.leaf[j + 1]; }
     b.d[K - 1] = __builtin_inff();
 }
 
 template <int K>
-__device__ __forceinline__ int32_t lb_node(const LeafBuf<K>& b, int j) {
-    int32_t r = b.node[0];
+__device__ __forceinline__ int32_t lb_leaf(const LeafBuf<K>& b, int j) {
+    int32_t r = b.leaf[0];
 #pragma unroll
-    for (int q = 1; q < K; ++q) r = (j == q) ? b.node[q] : r;
+    for (int q = 1; q < K; ++q) r = (j == q) ? b.leaf[q] : r;
     return r;
 }
 
 // One inner node of the derived-box table (engine.h DModel::inner).
 struct Inner {
     float lx, ly, lz, vx, vy, vz, hx, hy, hz;
-    int32_t child;   // children_start_position (node index of child 0)
+    int32_t leaf0;   // discovery rank of the first leaf child (leaf children are consecutive)
     int32_t parent;  // parent's inner id, -1 at the root
     uint32_t bm;     // (inner id of the first inner child << 8) | leaf-children mask
 };
@@ -208,7 +205,7 @@ __device__ __forceinline__ Inner load_inner(const float4_t* __restrict__ tab, in
     n.lx = a.x; n.ly = a.y; n.lz = a.z; n.vx = a.w;
     n.vy = b.x; n.vz = b.y; n.hx = b.z; n.hy = b.w;
     n.hz = c.x;
-    n.child = __float_as_int(c.y);
+    n.leaf0 = __float_as_int(c.y);
     n.parent = __float_as_int(c.z);
     n.bm = __float_as_uint(c.w);
     return n;
@@ -222,7 +219,7 @@ __device__ __forceinline__ Inner load_inner(const float4_t* __restrict__ tab, in
 // (aabb.h:29-93), hence the same bits, computed once per node instead of per child and with
 // no child box loads. Child k: x half = k >> 2, y half = (k >> 1) & 1, z half = k & 1.
 template <int K, bool COUNT>
-__device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, LeafBuf<K>& lb, int32_t& disc,
+__device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, LeafBuf<K>& lb,
                                                   int32_t& ncand, float bd, int32_t bi, Ctr& ct,
                                                   bool first_pass) {
     const float X0 = (n.lx - r.o.x) * r.inv.x, X1 = (n.vx - r.o.x) * r.inv.x, X2 = (n.hx - r.o.x) * r.inv.x;
@@ -257,10 +254,11 @@ __device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, 
             const float dis = !in ? 0.0f : (tmin > 0 ? tmin : (tmax > 0 ? tmax : 0.0f));
             if (dis > 0.0f) {
                 ++nodes_hit;
-                const int32_t id = disc++;
+                // the static discovery rank orders leaves exactly as this pass discovers them
+                const int32_t id = n.leaf0 + __popc(n.bm & ((1u << i) - 1u) & 0xFFu);
                 if (dis > bd || (dis == bd && id > bi)) {
                     ++ncand;
-                    lb_insert<K>(lb, dis, n.child + i, id);
+                    lb_insert<K>(lb, dis, id);
                 }
             }
         }
@@ -280,9 +278,9 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
     const bool first_pass = bi < 0;
     if constexpr (COUNT) ct.pass += 1;
     lb_clear<K>(lb);
-    int32_t disc = 0, ncand = 0;
+    int32_t ncand = 0;
     Inner cur = load_inner(tab, 0);
-    uint64_t lo = examine_inner<K, COUNT>(r, cur, lb, disc, ncand, bd, bi, ct, first_pass);
+    uint64_t lo = examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass);
     uint64_t hi = 0;
     uint32_t bm = cur.bm;
     int32_t parent = -1, lvl = 0;
@@ -295,7 +293,7 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
             const uint32_t innerm = ~bm & ((1u << s) - 1u);  // inner children before s
             const int32_t id = int32_t(bm >> 8) + __popc(innerm);
             cur = load_inner(tab, id);
-            const uint64_t cm = examine_inner<K, COUNT>(r, cur, lb, disc, ncand, bd, bi, ct, first_pass);
+            const uint64_t cm = examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass);
             ++lvl;
             if (lvl >= kMaskLevels) return -1;
             if (lvl < 8) lo |= cm << (8 * lvl);

@@ -135,13 +135,13 @@ __device__ __forceinline__ int32_t wf_store_pass(const WFParams& W, int32_t r, c
     const int32_t n = W.n;
     const int32_t nb = ncand < kLeafBuf ? ncand : kLeafBuf;
 #pragma unroll
-    for (int k = 0; k < kLeafBuf; ++k) W.ql[k * n + r] = lb.node[k];
+    for (int k = 0; k < kLeafBuf; ++k) W.ql[k * n + r] = lb.leaf[k];
     W.qd7[r] = lb.d[kLeafBuf - 1];
-    W.qi7[r] = lb.idx[kLeafBuf - 1];
+    W.qi7[r] = lb.leaf[kLeafBuf - 1];
     W.qpos[r] = 0;
     W.qnb[r] = nb;
     W.qnc[r] = ncand;
-    return nb > 0 ? lb.node[0] : -1;
+    return nb > 0 ? lb.leaf[0] : -1;
 }
 
 // bin + append: every lane of the wave calls it; lanes with leaf >= 0 join step `lst`
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_traverse(WFParams W, int32_t mode
                 if (root.children == 0) {  // root is a leaf: scan it alone (:344-361)
                     LeafBuf<kLeafBuf> lb;
                     lb_clear<kLeafBuf>(lb);
-                    lb.node[0] = 0;
+                    lb.leaf[0] = 0;
                     leaf = wf_store_pass(W, r, lb, 1);
                 } else {
                     LeafBuf<kLeafBuf> lb;

@@ -50,13 +50,14 @@ def algorithmic_bytes_per_ray(ctr):
 
 
 def cluster_bytes_per_ray(ctr):
-    """The clustered scan's own algorithmic bytes: ray in + hit out (36), the
-    reference traversal's box tests (28 each) and leaf records (8), cluster records (32), one
-    16-B normal+ac.z per screened primitive, 32 B more (a, ab, ac.xy) per full triangle test.
-    N_* counted live by the instrumented build of the same kernel on the same frame."""
+    """The clustered kernel's own algorithmic bytes per ray, in its own data layout (DESIGN.md
+    §6): ray in + hit out (36); one 48-B inner-node record per visit, shared by the 8 child boxes
+    it tests (6 per box test, re-walks included); 8 per leaf range; 32 per cluster record; the
+    screen's 6 (three f16) per screened primitive; a, ab, ac (36) per full triangle test. N_*
+    counted live by the instrumented build of the same kernel on the same frame."""
     n = ctr["n_rays"]
-    return (36.0 + 28.0 * ctr["n_box"] / n + 8.0 * ctr["n_leaf"] / n + 32.0 * ctr["cluster_boxes"] / n
-            + 16.0 * ctr["screened"] / n + 32.0 * ctr["n_tri"] / n)
+    return (36.0 + 6.0 * ctr["box_all"] / n + 8.0 * ctr["n_leaf"] / n + 32.0 * ctr["cluster_boxes"] / n
+            + 6.0 * ctr["screened"] / n + 36.0 * ctr["n_tri"] / n)
 
 
 def pmc_traffic(args, kernel_name="render_kernel"):
