@@ -795,14 +795,18 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                         nw[24 * cl + 16 + i / 2] |= uint32_t(h[2]) << (16 * (i & 1));
                     }
                 }
-                if (C.rec.empty()) C.rec.assign(8, 0.f);
-                if ((rc = dev_upload(c, C.rec.data(), C.rec.size() * sizeof(float), &p))) return rc;
+                // one 128-B block per cluster: record {lo, P}{hi, q}, then its 24 normal words
+                std::vector<uint32_t> blk(std::max<size_t>(1, ncl) * 4 * kClusterBlock, 0u);
+                for (size_t cl = 0; cl < ncl; ++cl) {
+                    std::memcpy(&blk[4 * kClusterBlock * cl], &C.rec[8 * cl], 8 * sizeof(float));
+                    std::memcpy(&blk[4 * kClusterBlock * cl + 8], &nw[24 * cl], 24 * sizeof(uint32_t));
+                }
+                if ((rc = dev_upload(c, blk.data(), blk.size() * sizeof(uint32_t), &p))) return rc;
                 dm.clus = static_cast<const float4_t*>(p);
+                dm.cnrm = reinterpret_cast<const uint4_t*>(dm.clus + 2);
                 C.range = by_rank(C.range);
                 if ((rc = dev_upload(c, C.range.data(), C.range.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cl_range = static_cast<const uint32_t*>(p);
-                if ((rc = dev_upload(c, nw.data(), nw.size() * sizeof(uint32_t), &p))) return rc;
-                dm.cnrm = static_cast<const uint4_t*>(p);
                 if ((rc = dev_upload(c, s0.data(), s0.size() * sizeof(float4_t), &p))) return rc;
                 dm.c0 = static_cast<const float4_t*>(p);
                 if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
@@ -811,7 +815,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 dm.c2 = static_cast<const c2_t*>(p);
                 if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cface = static_cast<const uint32_t*>(p);
-                c->nclusters += int64_t(C.rec.size() / 8);
+                c->nclusters += int64_t(ncl);
             }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
             dm.nodes = static_cast<const DNode*>(p);
@@ -970,6 +974,67 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     const int wave = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(launch_render(c, P, wave, s));
+    HIPCHK(hipEventRecord(c->ev_stop, s));
+    HIPCHK(hipEventRecord(c->ev_done, s));
+    c->have_render = true;
+    c->last_stream = s;
+    c->last_ntiles = ntiles;
+    return ATR_OK;
+}
+
+int atr_render_start_frames(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                            const atr_frame* fr, int32_t nframes, int64_t frame_stride, uint64_t seed, void* stream,
+                            int32_t variant) {
+    if (!c || !cam || !fr || !fr->framebuffer || ntiles < 0 || (ntiles && !tiles) || nframes < 1 || nframes > 64)
+        return ATR_E_INVALID;
+    if (cam->width <= 0 || cam->height <= 0 || cam->width > (1 << 16) || cam->height > (1 << 16)) return ATR_E_INVALID;
+    if (fr->layout != ATR_LAYOUT_IMAGE && fr->layout != ATR_LAYOUT_PACKED) return ATR_E_INVALID;
+    if (variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
+    if (!bs) return rc;
+    const int64_t per_frame = fr->layout == ATR_LAYOUT_IMAGE ? int64_t(cam->width) * cam->height : bs->packed_pixels;
+    if (nframes > 1 && frame_stride < per_frame) return ATR_E_INVALID;
+    const int32_t nb = int32_t(bs->host.size());
+    if (int64_t(nb) * nframes > (int64_t(1) << 30)) return ATR_E_INVALID;
+    c->prog_active = false;
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.blocks = static_cast<const DBlock*>(bs->dev.p);
+    P.layout = fr->layout;
+    P.framebuffer = fr->framebuffer;
+    P.hit_face = fr->hit_face;
+    P.hit_t = fr->hit_t;
+    P.rgb = fr->rgb;
+    P.ray_casts = fr->ray_casts;
+    P.traced_rays = fr->traced_rays;
+    P.error_flag = c->d_error;
+    P.xcd_chunk = xcd_chunk();
+    const int sched = auto_sched(variant, *cam);
+    HIPCHK(hipEventRecord(c->ev_start, s));
+    if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
+        P.nblocks = nb * nframes;
+        P.frame_blocks = nb;
+        P.frame_stride = frame_stride;
+        HIPCHK(launch_render(c, P, sched, s));
+    } else {  // persistent lanes take pixels from a queue: one launch per frame
+        P.nblocks = nb;
+        for (int32_t f = 0; f < nframes; ++f) {
+            const size_t o = size_t(f) * size_t(frame_stride);
+            P.framebuffer = fr->framebuffer + o;
+            P.hit_face = fr->hit_face ? fr->hit_face + o : nullptr;
+            P.hit_t = fr->hit_t ? fr->hit_t + o : nullptr;
+            P.rgb = fr->rgb ? fr->rgb + 3 * o : nullptr;
+            P.ray_casts = fr->ray_casts ? fr->ray_casts + o : nullptr;
+            HIPCHK(launch_render(c, P, sched, s));
+        }
+    }
     HIPCHK(hipEventRecord(c->ev_stop, s));
     HIPCHK(hipEventRecord(c->ev_done, s));
     c->have_render = true;

@@ -69,7 +69,7 @@ __device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint3
 // leaf: padded box tests, then the screen and the full tests of its primitives.
 template <bool COUNT>
 __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
-                                             const uint4_t* pre, LeafHit& h, Ctr& ct) {
+                                             LeafHit& h, Ctr& ct) {
     const float ax = fabsf(r.inv.x), ay = fabsf(r.inv.y), az = fabsf(r.inv.z);
     const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
     const float fx = fmaxf(fabsf(lo.x - r.o.x), fabsf(hi.x - r.o.x));
@@ -113,12 +113,11 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     const h2 dxy = {(_Float16)r.d.x, (_Float16)r.d.y};
     const _Float16 hz = (_Float16)r.d.z;
     const h2 dz_lo = {hz, (_Float16)0.0f}, dz_hi = {(_Float16)0.0f, hz};
-    const uint4_t* nb = m.cnrm + 6 * size_t(c);
+    const uint4_t* nb = m.cnrm + kClusterBlock * size_t(c);
     const float nq = -q;
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8) {  // eight primitives per step: (nx, ny) x 8, nz x 8
-        const uint4_t a0 = (pre && g == 0) ? pre[0] : nb[g / 4], a1 = (pre && g == 0) ? pre[1] : nb[g / 4 + 1],
-                      z = (pre && g == 0) ? pre[2] : nb[4 + g / 8];
+        const uint4_t a0 = nb[g / 4], a1 = nb[g / 4 + 1], z = nb[4 + g / 8];
         const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
 #pragma unroll
@@ -151,35 +150,21 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     }
 }
 
-// Clusters [c, cend) of one leaf, the next cluster's record (and, with ATR_NRM_PREFETCH, its
-// first eight screen normals) in flight while the current one is screened.
+// Clusters [c, cend) of one leaf, the next cluster's record in flight while the current one is
+// screened (the record shares its 128-B block with the cluster's screen normals, so that load
+// also brings the normals the screen reads next).
 template <bool COUNT>
 __device__ __forceinline__ void cluster_range(const Ray& r, const DModel& m, uint32_t c, uint32_t cend, LeafHit& h,
                                               Ctr& ct) {
     if (c >= cend) return;
-    float4_t nlo = m.clus[2 * c], nhi = m.clus[2 * c + 1];
-#ifdef ATR_NRM_PREFETCH
-    uint4_t np[3] = {m.cnrm[6 * size_t(c)], m.cnrm[6 * size_t(c) + 1], m.cnrm[6 * size_t(c) + 4]};
-#endif
+    float4_t nlo = m.clus[kClusterBlock * size_t(c)], nhi = m.clus[kClusterBlock * size_t(c) + 1];
     for (; c < cend; ++c) {
         const float4_t lo = nlo, hi = nhi;
-#ifdef ATR_NRM_PREFETCH
-        const uint4_t cp[3] = {np[0], np[1], np[2]};
-#endif
         if (c + 1 < cend) {
-            nlo = m.clus[2 * c + 2];
-            nhi = m.clus[2 * c + 3];
-#ifdef ATR_NRM_PREFETCH
-            np[0] = m.cnrm[6 * size_t(c + 1)];
-            np[1] = m.cnrm[6 * size_t(c + 1) + 1];
-            np[2] = m.cnrm[6 * size_t(c + 1) + 4];
-#endif
+            nlo = m.clus[kClusterBlock * size_t(c + 1)];
+            nhi = m.clus[kClusterBlock * size_t(c + 1) + 1];
         }
-#ifdef ATR_NRM_PREFETCH
-        cluster_step<COUNT>(r, m, c, lo, hi, cp, h, ct);
-#else
-        cluster_step<COUNT>(r, m, c, lo, hi, nullptr, h, ct);
-#endif
+        cluster_step<COUNT>(r, m, c, lo, hi, h, ct);
     }
 }
 

@@ -19,6 +19,7 @@ namespace atr {
 struct alignas(16) float4_t { float x, y, z, w; };
 struct alignas(16) uint4_t { uint32_t x, y, z, w; };
 struct alignas(8) float2_t { float x, y; };
+struct alignas(8) uint2_t { uint32_t x, y; };
 #ifdef ATR_C2_WIDE
 using c2_t = float4_t;  // experiment: 16-B third word
 #else
@@ -32,6 +33,7 @@ constexpr int kMaskLevels = 16;                   // traversal mask-stack depth 
 constexpr int kMaxMaterials = 32;
 constexpr int kMaxModels = 8;
 constexpr int kMaxClusterSize = 16;  // primitive slots per leaf cluster (ATR_CLUSTER_SIZE <= this)
+constexpr int kClusterBlock = 8;     // 16-B words per cluster block: record (2), screen normals (6)
 
 struct V3 { float x, y, z; };
 ATR_HD V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -113,7 +115,8 @@ struct DModel {
     const uint32_t* tface;
     // leaf clusters, 2 float4 per cluster: {lo.xyz, bound of |ab||ac| with
     // (n - 1) in its low 5 mantissa bits}, {hi.xyz, q}; cl_range = first cluster, count per
-    // node. Cluster c owns the primitive slots [16 c, 16 c + n): cnrm = 6 uint4 of its normals
+    // node. Cluster c owns the primitive slots [16 c, 16 c + n) and the 128-B block clus[8 c ..]:
+    // its record (2 words), then (cnrm = clus + 2) 6 words of its screen normals
     // n = ab x ac as f16 integer multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
     // c1 = {ab.yz, ac.xy}, c2 = {ac.z, bits(leaf rank)}, cface = face index
     const float4_t* clus;
@@ -176,6 +179,8 @@ struct RenderParams {
     int32_t xcd_chunk;  // 0: contiguous block range per XCD; k > 0: k-workgroup chunks dealt round-robin
     uint32_t* queue;    // PERSIST: 8 zeroed per-XCD work-queue heads (persist.hip)
     int32_t qchunk;     // PERSIST: 8x8 cells per queue chunk
+    int32_t frame_blocks;  // > 0: nblocks = frames x frame_blocks, one launch renders every frame
+    int64_t frame_stride;  // output elements between consecutive frames (rgb: 3 x this)
 };
 
 }  // namespace atr

@@ -189,8 +189,9 @@ __device__ __forceinline__ void begin_leaf(Lane<K>& L, const DModel& m, Ctr& ct)
     const int32_t leaf = L.lb.leaf[0];
     L.bd = L.lb.d[0];
     L.bi = L.lb.leaf[0];
-    L.c = m.cl_range[2 * leaf];
-    const uint32_t n = m.cl_range[2 * leaf + 1];
+    const uint2_t cr = load_range(m.cl_range, leaf);
+    L.c = cr.x;
+    const uint32_t n = cr.y;
     L.cend = L.c + n;
     L.h.improved = false;
     L.h.rank = -1;

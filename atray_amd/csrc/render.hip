@@ -102,8 +102,10 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
     uint32_t slot = 0xFFFFFFFFu;
     const uint32_t* range = CL ? m.cl_range : m.leaf_range;
     auto scan = [&](int32_t leaf) -> bool {
-        if constexpr (CL)
-            return scan_leaf_clusters<COUNT>(r, m, range[2 * leaf], range[2 * leaf + 1], h.t, slot, h.u, h.v, ct);
+        if constexpr (CL) {
+            const uint2_t cr = load_range(range, leaf);
+            return scan_leaf_clusters<COUNT>(r, m, cr.x, cr.y, h.t, slot, h.u, h.v, ct);
+        }
         else
             return scan_leaf_lane<COUNT>(r, m, range[2 * leaf], range[2 * leaf + 1], h.t, slot, h.u, h.v, ct);
     };
@@ -496,8 +498,13 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     const int b = remap_xcd(blockIdx.x, gridDim.x, P.xcd_chunk) * NW + wave;
     if (SCHED != SCHED_TILE4 && SCHED != SCHED_TILE8 && b >= P.nblocks) return;  // whole wavefront
     const bool in_range = b < P.nblocks;
+    // several frames per launch, interleaved: block b renders block b / nf of frame b % nf, so the
+    // frames advance through the block list together (each frame's slow cells start early, and
+    // neighbouring workgroups trace the same cells' rays)
+    const int32_t nf = P.frame_blocks > 0 ? P.nblocks / P.frame_blocks : 1;
+    const int32_t fidx = b % nf;
     DBlock blk;
-    if (in_range) blk = P.blocks[b];
+    if (in_range) blk = P.blocks[b / nf];
     else { blk.x0 = 0; blk.y0 = 0; blk.mask_lo = 0; blk.mask_hi = 0; blk.out_base = 0; }
     const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
     const bool active = (mask >> lane) & 1;
@@ -554,6 +561,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         size_t o;
         if (P.layout == ATR_LAYOUT_PACKED) o = size_t(blk.out_base) + __popcll(mask & ((uint64_t(1) << lane) - 1));
         else o = size_t(y) * size_t(cm.width) + size_t(x);
+        o += size_t(fidx) * size_t(P.frame_stride);
         P.framebuffer[o] = b8 | (g8 << 8) | (r8 << 16);  // Set_Pixel (texture.h:27-38)
         if (P.hit_face) P.hit_face[o] = hit_face;
         if (P.hit_t) P.hit_t[o] = hit_t;

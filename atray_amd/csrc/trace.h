@@ -146,6 +146,11 @@ __device__ __forceinline__ bool scan_leaf(const Ray& r, const DTri* __restrict__
 // ------------------------------------------------------------------ leaf order buffer
 constexpr int kLeafBuf = 8;  // sorted leaves held per ray between DFS passes
 
+// {first, count} of leaf `leaf` in a per-leaf range table (one 8-B load)
+__device__ __forceinline__ uint2_t load_range(const uint32_t* __restrict__ range, int32_t leaf) {
+    return reinterpret_cast<const uint2_t*>(range)[leaf];
+}
+
 template <int K>
 struct LeafBuf {
     float d[K];

@@ -92,7 +92,7 @@ EXPORTS = [
     "atr_render_counters", "atr_render_tile_costs", "atr_render_wave_trace", "atr_balance_shard_tiles",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
-    "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp",
+    "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
 ]
 
 _lib = None
@@ -144,6 +144,8 @@ def lib():
         "atr_render_start_progressive": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32, i32],
                                          C.c_int),
         "atr_write_bmp": ([vp, i32, i32, C.c_char_p, C.c_char_p, i32], C.c_int),
+        "atr_render_start_frames": ([vp, P(atr_camera), vp, i32, P(atr_frame), i32, i64, C.c_uint64, vp, i32],
+                                    C.c_int),
         "atr_last_kernel_ms": ([vp, P(C.c_float)], C.c_int),
         "atr_device_alloc": ([vp, C.c_size_t, P(vp)], C.c_int),
         "atr_device_free": ([vp, vp], C.c_int),
@@ -381,6 +383,15 @@ class Engine:
                                                  C.byref(frame), C.c_uint64(seed & (2**64 - 1)),
                                                  C.c_void_p(stream) if stream else None, int(variant),
                                                  int(tiles_per_launch)), "progressive render start")
+
+    def render_start_frames(self, cam, tiles, frame: atr_frame, nframes, frame_stride, seed, stream=None,
+                            variant=ATR_KERNEL_AUTO):
+        """nframes renders in one launch; frame f's outputs at f * frame_stride elements."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_render_start_frames(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.byref(frame),
+                                            int(nframes), int(frame_stride), C.c_uint64(seed & (2**64 - 1)),
+                                            C.c_void_p(stream) if stream else None, int(variant)),
+              "render start frames")
 
     def counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
         arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)

@@ -45,6 +45,18 @@ class ShardPlan:
         return E.packed_pixel_map(self.tiles[rank], self.width, self.height)
 
 
+def assembly_index(plan: ShardPlan) -> np.ndarray:
+    """Destination pixel of every slot of the gathered [world x max_size] buffer (rank r's packed
+    pixels at r * max_size); padding slots point at a trash pixel width * height just past the
+    image, so the whole frame assembles with one index_copy_ into a (W * H + 1) buffer."""
+    n = plan.world * plan.max_size
+    dst = np.full(n, plan.width * plan.height, np.int64)
+    for r in range(plan.world):
+        m = plan.pixel_map(r) if len(plan.tiles[r]) else np.zeros(0, np.int64)
+        dst[r * plan.max_size:r * plan.max_size + len(m)] = m
+    return dst
+
+
 def tile_costs(eng, cam, width: int, height: int, side: int, seed: int) -> np.ndarray:
     """Measured cost (GPU shader clocks) of every grid tile: one calibration render."""
     return eng.tile_costs(cam, E.shard_grid(width, height, side), seed)

@@ -22,12 +22,14 @@ import csv
 import glob
 import json
 import os
+import re
 import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
 
 SEED = 0x853C49E6748FEA9B
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -73,6 +75,7 @@ def pmc_traffic(args, kernel_name="render_kernel"):
         os.makedirs(d, exist_ok=True)
         cmd = [exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+               "--frames-per-launch", "1", "--streams", "1",
                "--config", args.config, "--variant", args.variant, "--no-cpu-baseline", "--no-pmc"]
         env = dict(os.environ)
         env.pop("RANK", None)
@@ -86,7 +89,10 @@ def pmc_traffic(args, kernel_name="render_kernel"):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if kernel_name in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    name = row.get("Kernel_Name", "")
+                    # one-frame launches of the product kernel (not the instrumented COUNT build)
+                    if kernel_name in name and not re.search(r"render_kernel<\d+, true", name) \
+                            and row.get("Counter_Name") == ctr:
                         vals.append(float(row["Counter_Value"]))
         if not vals:
             return None, f"no {ctr} rows"
@@ -116,23 +122,32 @@ def cpu_baseline(asset, W, H, spp, bounces, use_tree, seconds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps"])
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
-    ap.add_argument("--streams", type=int, default=3,
-                    help="frames in flight (one HIP stream each); 1 = strictly one frame at a time")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="launches in flight (one HIP stream each)")
+    ap.add_argument("--frames-per-launch", type=int, default=8,
+                    help="frames rendered by one launch (atr_render_start_frames); 1 = one frame per launch")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
                     help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
     ap.add_argument("--check", action="store_true",
                     help="rank 0: compare the assembled frame with a one-launch full-frame render")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES floor for this process (0 = leave the environment alone)")
     args = ap.parse_args()
+    # Frames in flight run on separate HIP streams; HIP maps a process's streams onto
+    # GPU_MAX_HW_QUEUES hardware queues (default 4, shared with RCCL's streams), and streams on
+    # one queue serialize. Read at HIP initialization, so set before torch loads.
+    if args.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
     import numpy as np
     import torch
@@ -180,82 +195,91 @@ def main():
         plan = S.ShardPlan(W, H, world, args.side)
     sizes, maxn = plan.sizes, plan.max_size
     tiles = E.tiles_array(plan.tiles[rank])
-    # S frames in flight, one HIP stream and one set of output buffers each: frame k renders on
-    # stream k % S while earlier frames finish, are gathered (N > 1) and assembled on rank 0
-    S_ = max(1, args.streams)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S_ - 1)]
-    images = [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(S_)] if rank == 0 else None
-    packed = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(S_)] if world > 1 else None
+    # Frames in flight: launch j renders frames jF .. jF+F-1 (F = --frames-per-launch, one grid:
+    # a frame's slow cells overlap the other frames') on stream j % S (S = --streams, output
+    # buffers per stream); for N > 1 the launch's F packed frames are gathered to rank 0 in ONE
+    # gather on that stream and assembled there with ONE index_copy_ while later launches run.
+    S_, F_ = max(1, args.streams), max(1, args.frames_per_launch)
+    # frame slots on streams of their own (not the null stream, which HIP orders against the
+    # process's blocking streams)
+    streams = [torch.cuda.Stream(dev) for _ in range(S_)]
+    npf = W * H if world == 1 else maxn  # output elements per frame (stride between frames)
+    outbuf = [torch.zeros(F_ * npf, dtype=torch.int32, device=dev) for _ in range(S_)]
     on_host = world > 1 and backend != "nccl"
-    gather = [[torch.zeros(maxn, dtype=torch.int32, device="cpu" if on_host else dev) for _ in range(world)]
-              for _ in range(S_)] if (rank == 0 and world > 1) else None
+    images = None
+    if world == 1:
+        images = [outbuf[q][f * npf:(f + 1) * npf] for q in range(S_) for f in range(F_)]
+    elif rank == 0:
+        # per stream slot: every rank's F packed frames [world x F x maxn]; one index_copy_ through
+        # the plan's assembly index (padding -> a trash pixel past each frame) writes F images
+        big = [torch.zeros(world * F_ * maxn, dtype=torch.int32, device="cpu" if on_host else dev)
+               for _ in range(S_)]
+        gather = [[b_[r * F_ * maxn:(r + 1) * F_ * maxn] for r in range(world)] for b_ in big]
+        one = S.assembly_index(plan).reshape(world, 1, maxn)
+        dst_all = one + (np.arange(F_, dtype=np.int64) * (W * H + 1)).reshape(1, F_, 1)
+        dst_idx = torch.from_numpy(np.ascontiguousarray(dst_all).ravel()).to(dev)
+        images_ext = [torch.zeros(F_ * (W * H + 1), dtype=torch.int32, device=dev) for _ in range(S_)]
+        images = [im[f * (W * H + 1):f * (W * H + 1) + W * H] for im in images_ext for f in range(F_)]
+        staging = torch.zeros(world * F_ * maxn, dtype=torch.int32, device=dev) if on_host else None
     traced = torch.zeros(1, dtype=torch.int64, device=dev)
-
-    def frame_of(slot, count=False):
-        if world == 1:
-            fb, layout = images[slot], E.ATR_LAYOUT_IMAGE
-        else:
-            fb, layout = packed[slot], E.ATR_LAYOUT_PACKED
-        return E.atr_frame(layout, fb.data_ptr(), None, None, None, None, traced.data_ptr() if count else None)
-
-    frames = [frame_of(q) for q in range(S_)]
-    other_tiles = [E.tiles_array(t) for t in plan.tiles]
-    staging = [torch.zeros(maxn, dtype=torch.int32, device=dev) for _ in range(world)] if on_host and rank == 0 else None
+    layout = E.ATR_LAYOUT_IMAGE if world == 1 else E.ATR_LAYOUT_PACKED
+    frames = [E.atr_frame(layout, outbuf[q].data_ptr(), None, None, None, None, None) for q in range(S_)]
     pending = {}
 
-    def assemble(k):
-        """Frame k's gather done (its stream waits on it); rank 0 scatters every rank's packed
-        pixels into that slot's image, on the frame's stream."""
-        q = k % S_
-        work = pending.pop(k)
+    def assemble(j):
+        """Launch j's gather done (its stream waits on it); rank 0 scatters every rank's packed
+        frames into that slot's images, on the launch's stream."""
+        q = j % S_
+        work = pending.pop(j)
         with torch.cuda.stream(streams[q]):
             if work is not None:
                 work.wait()
             if rank == 0:
-                for r in range(world):
-                    src = gather[q][r]
-                    if on_host:
-                        staging[r].copy_(src, non_blocking=False)
-                        src = staging[r]
-                    eng.unpack(other_tiles[r], W, src.data_ptr(), images[q].data_ptr(), streams[q].cuda_stream)
-
-    def step(k, fr):
-        q = k % S_
-        eng.render_start(cam, tiles, fr, SEED, stream=streams[q].cuda_stream, variant=variant)
-        if world > 1:
-            with torch.cuda.stream(streams[q]):
-                buf = packed[q]
+                src = big[q]
                 if on_host:
-                    torch.cuda.synchronize()
-                    buf = buf.cpu()
-                pending[k] = dist.gather(buf, gather[q] if rank == 0 else None, dst=0, async_op=True)
-            if k - S_ + 1 in pending:
-                assemble(k - S_ + 1)  # the oldest frame in flight, before its slot is reused
+                    staging.copy_(src, non_blocking=False)
+                    src = staging
+                images_ext[q].index_copy_(0, dst_idx, src)
 
-    def flush():
-        for k in sorted(pending):
-            assemble(k)
+    def launch(j, nf, fr=None):
+        q = j % S_
+        if j - S_ in pending:
+            assemble(j - S_)  # before this slot's buffers are reused
+        eng.render_start_frames(cam, tiles, fr or frames[q], nf, npf, SEED, stream=streams[q].cuda_stream,
+                                variant=variant)
+        if world == 1:
+            return
+        with torch.cuda.stream(streams[q]):
+            buf = outbuf[q]
+            if on_host:
+                torch.cuda.synchronize()
+                buf = buf.cpu()
+            pending[j] = dist.gather(buf, gather[q] if rank == 0 else None, dst=0, async_op=True)
 
+    def run_steps(n):
+        for j in range((n + F_ - 1) // F_):
+            launch(j, min(F_, n - j * F_))
+        for j in sorted(pending):
+            assemble(j)
+
+    torch.cuda.synchronize()  # buffers were zero-filled on the current stream
     # rays per frame (all ranks): counted by the kernel (every get_intersection_data call)
-    step(0, frame_of(0, count=True))
-    flush()
+    launch(0, 1, E.atr_frame(layout, outbuf[0].data_ptr(), None, None, None, None, traced.data_ptr()))
+    for j in sorted(pending):
+        assemble(j)
     torch.cuda.synchronize()
     rays_t = traced.clone() if backend == "nccl" or world == 1 else traced.cpu()
     if world > 1:
         dist.all_reduce(rays_t)
     rays_per_step = int(rays_t.item())
 
-    for k in range(args.warmup):
-        step(k, frames[k % S_])
-    flush()
+    run_steps(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k, frames[k % S_])
-    flush()
+    run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -284,7 +308,9 @@ def main():
         fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, ref.data_ptr(), None, None, None, None, None)
         eng.render_start(cam, [[0, 0, W - 1, H - 1]], fr, SEED, stream=stream)
         torch.cuda.synchronize()
-        check = sum(int((ref != im).sum().item()) for im in images)
+        # images holding a frame: stream slot j % S, position f of launch j
+        used = sorted({((k // F_) % S_) * F_ + k % F_ for k in range(max(args.steps, args.warmup))})
+        check = sum(int((ref != images[q]).sum().item()) for q in used)
 
     if rank == 0:
         value = rays_per_step * args.steps / elapsed / 1e6
@@ -297,7 +323,9 @@ def main():
                                       f"{'octree' if use_tree else 'brute-force'}",
                           "rays_per_step": rays_per_step, "shard_tile": args.side,
                           "parallelism": f"tiles{world}", "kernel": args.variant,
-                          "plan": args.plan if world > 1 else "single", "frames_in_flight": args.streams,
+                          "plan": args.plan if world > 1 else "single",
+                          "frames_in_flight": args.streams * args.frames_per_launch,
+                          "streams": args.streams, "frames_per_launch": args.frames_per_launch,
                           "shard_pixels": [int(x) for x in sizes]}}
         if check is not None:
             out["check_mismatched_pixels"] = check

@@ -181,6 +181,15 @@ int atr_render_start_progressive(atr_ctx* ctx, const atr_camera* cam, const atr_
 /* Like atr_render_start with an explicit kernel variant. */
 int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         const atr_frame* frame, uint64_t seed, void* stream, int32_t variant);
+/* Frames in flight in one launch (throughput, e.g. a live view rendering ahead): nframes renders
+   of the same camera and tiles; frame f's outputs start frame_stride elements after frame f-1's
+   (rgb: 3 x frame_stride floats; frame_stride >= the layout's pixels per frame). The cell
+   schedules run all frames as one grid, so one frame's slow cells overlap the next frame's;
+   PERSIST (multi-bounce AUTO) launches once per frame. Every frame equals atr_render_start_ex's
+   output. */
+int atr_render_start_frames(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                            const atr_frame* frame, int32_t nframes, int64_t frame_stride, uint64_t seed,
+                            void* stream, int32_t variant);
 /* Diagnostic, synchronous: an instrumented render of the same work that returns
    [0] traced rays, [1] box tests, [2] triangle tests, [3] leaves scanned -- the reference's own
    per-ray work on this input (kd_tree.cpp:337-465) for every variant but CLUSTER, whose [2]

@@ -169,6 +169,52 @@ def test_renderer_api_start_wait(eng):
     assert info.jobs_done == len(tiles) == 40
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("bounces", [1, 3])
+def test_frames_per_launch_equal_single_renders(eng, variant, bounces):
+    """atr_render_start_frames: every frame of a multi-frame launch (outputs frame_stride apart,
+    image and packed layouts) equals the single-frame render."""
+    upload(eng, "Monkey", True)
+    W, H = 96, 56
+    cam = E.camera(W, H, 2, bounces)
+    tiles = E.make_tiles(W, H, 4)
+    if variant == E.ATR_KERNEL_WAVEFRONT:
+        with pytest.raises(E.AtrError):
+            fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            eng.render_start_frames(cam, tiles, E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None,
+                                                             None, None), 2, W * H, SEED, variant=variant)
+        return
+    for layout in (E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED):
+        want = run(eng, cam, tiles=tiles, layout=layout, variant=variant)
+        n = W * H if layout == E.ATR_LAYOUT_IMAGE else E.packed_size(tiles)
+        F, stride = 3, n + 37
+        fb = torch.full((F * stride,), 0x7F7F7F7F, dtype=torch.int32, device="cuda")
+        face = torch.full((F * stride,), -7, dtype=torch.int32, device="cuda")
+        t = torch.zeros(F * stride, dtype=torch.float32, device="cuda")
+        rgb = torch.zeros(3 * F * stride, dtype=torch.float32, device="cuda")
+        casts = torch.full((F * stride,), -1, dtype=torch.int32, device="cuda")
+        traced = torch.zeros(1, dtype=torch.int64, device="cuda")
+        fr = E.atr_frame(layout, fb.data_ptr(), face.data_ptr(), t.data_ptr(), rgb.data_ptr(), casts.data_ptr(),
+                         traced.data_ptr())
+        torch.cuda.synchronize()
+        eng.render_start_frames(cam, tiles, fr, F, stride, SEED, stream=torch.cuda.current_stream().cuda_stream,
+                                variant=variant)
+        rc, _ = eng.wait()
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert int(traced.item()) == F * want["traced"]
+        for f in range(F):
+            sl = slice(f * stride, f * stride + n)
+            assert np.array_equal(fb[sl].cpu().numpy().view(np.uint32), want["fb"].ravel())
+            assert np.array_equal(face[sl].cpu().numpy().view(np.uint32), want["face"].ravel())
+            assert np.array_equal(t[sl].cpu().numpy().view(np.uint32), want["t"].ravel().view(np.uint32))
+            assert np.array_equal(casts[sl].cpu().numpy().view(np.uint32), want["casts"].ravel())
+            got_rgb = rgb[3 * f * stride:3 * f * stride + 3 * n].cpu().numpy()
+            assert np.array_equal(got_rgb.view(np.uint32), want["rgb"].ravel().view(np.uint32))
+            if f + 1 < F:  # the gap between frames is untouched
+                assert (fb[f * stride + n:(f + 1) * stride].cpu().numpy() == 0x7F7F7F7F).all()
+
+
 def test_renderer_api_progressive_live_view(eng):
     """Live view (app.cpp:162-186): tiles finish in groups while the render runs; every pixel
     of a tile reported done is final, and the finished frame equals the one-shot render."""

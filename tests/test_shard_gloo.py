@@ -103,7 +103,7 @@ def _bench_worker(rank, world, port, out_path):
 
     from atray_amd import engine as E
     from atray_amd.assets import CENTERS, asset_path
-    from atray_amd.shard import ShardPlan, scatter_host
+    from atray_amd.shard import ShardPlan, assembly_index
     from oracle import oracle as O
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -115,8 +115,18 @@ def _bench_worker(rank, world, port, out_path):
     plan = ShardPlan.balanced(costs, W, H, world, side, rank0_extra=0.1)
     m = plan.pixel_map(rank)
     packed = [torch.zeros(plan.max_size, dtype=torch.int64) for _ in range(2)]
-    gather = [[torch.zeros(plan.max_size, dtype=torch.int64) for _ in range(world)] for _ in range(2)]
+    # as bench.py: gather into views of one [world x max_size] tensor, assemble with one
+    # index_copy_ through the plan's assembly index (padding -> trash pixel W * H)
+    big = [torch.zeros(world * plan.max_size, dtype=torch.int64) for _ in range(2)]
+    gather = [[b[r * plan.max_size:(r + 1) * plan.max_size] for r in range(world)] for b in big]
+    dst = torch.from_numpy(assembly_index(plan))
     pending, frames = {}, []
+
+    def assemble(q):
+        img = torch.zeros(W * H + 1, dtype=torch.int64)
+        img.index_copy_(0, dst, big[q])
+        return img[:W * H].numpy().reshape(H, W)
+
     for k in range(5):
         packed[k % 2].zero_()
         packed[k % 2][:len(m)] = torch.from_numpy(face.ravel()[m].astype(np.int64) + k)
@@ -124,10 +134,10 @@ def _bench_worker(rank, world, port, out_path):
         if k - 1 in pending:
             pending.pop(k - 1).wait()
             if rank == 0:
-                frames.append(scatter_host([t.numpy() for t in gather[(k - 1) % 2]], plan))
+                frames.append(assemble((k - 1) % 2))
     pending.pop(4).wait()
     if rank == 0:
-        frames.append(scatter_host([t.numpy() for t in gather[0]], plan))
+        frames.append(assemble(0))
         np.save(out_path, np.stack(frames))
     dist.barrier()
     dist.destroy_process_group()

@@ -9,7 +9,7 @@ mkdir -p $O
 timeout -k 10 600 python bench.py > $O/bench_c3.log 2>&1 || exit 1
 grep '^{' $O/bench_c3.log > $O/bench_c3.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof -o bench -- \
-  python3 bench.py --steps 20 --warmup 3 --streams 1 --no-cpu-baseline --no-pmc > $O/rocprof_bench.log 2>&1 || exit 1
+  python3 bench.py --steps 20 --warmup 3 --streams 1 --frames-per-launch 1 --no-cpu-baseline --no-pmc > $O/rocprof_bench.log 2>&1 || exit 1
 timeout -k 10 400 python bench.py --config c4 --steps 3 --warmup 1 --no-pmc --no-cpu-baseline > $O/bench_c4.log 2>&1 || exit 1
 grep '^{' $O/bench_c4.log > $O/bench_c4.json
 ATR_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
