@@ -800,6 +800,43 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 for (size_t cl = 0; cl < ncl; ++cl) {
                     std::memcpy(&blk[4 * kClusterBlock * cl], &C.rec[8 * cl], 8 * sizeof(float));
                     std::memcpy(&blk[4 * kClusterBlock * cl + 8], &nw[24 * cl], 24 * sizeof(uint32_t));
+                    // bounding spheres (cluster.h, sphere filter): centre as u8 steps of the box
+                    // extent per axis, radius in u8 steps of the largest extent, rounded so the
+                    // decoded sphere holds the triangle the test sees (a, a + ab, a + ac)
+                    const float* rc = &C.rec[8 * cl];
+                    uint32_t first, pw;
+                    std::memcpy(&pw, &rc[3], 4);
+                    std::memcpy(&first, &rc[7], 4);
+                    (void)first;
+                    const uint32_t n = (pw & 31u) + 1u;
+                    const double ext[3] = {double(rc[4]) - rc[0], double(rc[5]) - rc[1], double(rc[6]) - rc[2]};
+                    const double emax = std::max(ext[0], std::max(ext[1], ext[2]));
+                    for (uint32_t i = 0; i < n; ++i) {
+                        const size_t slot = cl * kMaxClusterSize + i;
+                        const float4_t q0 = s0[slot], q1 = s1[slot];
+                        const double a[3] = {q0.x, q0.y, q0.z};
+                        const double ab[3] = {q0.w, q1.x, q1.y}, ac[3] = {q1.z, q1.w, double(s2[slot].x)};
+                        const double v[3][3] = {{a[0], a[1], a[2]},
+                                                {a[0] + ab[0], a[1] + ab[1], a[2] + ab[2]},
+                                                {a[0] + ac[0], a[1] + ac[1], a[2] + ac[2]}};
+                        uint32_t u[3];
+                        double cen[3];
+                        for (int ax = 0; ax < 3; ++ax) {
+                            const double cc = (v[0][ax] + v[1][ax] + v[2][ax]) / 3.0;
+                            const double t = ext[ax] > 0 ? (cc - rc[ax]) / ext[ax] * 255.0 : 0.0;
+                            u[ax] = uint32_t(std::min(255.0, std::max(0.0, std::round(t))));
+                            cen[ax] = double(rc[ax]) + double(u[ax]) * (ext[ax] / 255.0);
+                        }
+                        double rr = 0;
+                        for (int j = 0; j < 3; ++j) {
+                            double d2 = 0;
+                            for (int ax = 0; ax < 3; ++ax) d2 += (v[j][ax] - cen[ax]) * (v[j][ax] - cen[ax]);
+                            rr = std::max(rr, std::sqrt(d2));
+                        }
+                        const double step = emax > 0 ? emax / 255.0 : 1.0;
+                        const uint32_t rq = uint32_t(std::min(255.0, std::ceil(rr / step * (1.0 + 1e-6)) + 1.0));
+                        blk[4 * kClusterBlock * cl + 32 + i] = u[0] | (u[1] << 8) | (u[2] << 16) | (rq << 24);
+                    }
                 }
                 if ((rc = dev_upload(c, blk.data(), blk.size() * sizeof(uint32_t), &p))) return rc;
                 dm.clus = static_cast<const float4_t*>(p);

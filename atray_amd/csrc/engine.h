@@ -33,7 +33,8 @@ constexpr int kMaskLevels = 16;                   // traversal mask-stack depth 
 constexpr int kMaxMaterials = 32;
 constexpr int kMaxModels = 8;
 constexpr int kMaxClusterSize = 16;  // primitive slots per leaf cluster (ATR_CLUSTER_SIZE <= this)
-constexpr int kClusterBlock = 8;     // 16-B words per cluster block: record (2), screen normals (6)
+constexpr int kClusterBlock = 16;    // 16-B words per cluster block: record (2), screen normals (6),
+                                     // bounding spheres (4), spare (4)
 
 struct V3 { float x, y, z; };
 ATR_HD V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -115,8 +116,9 @@ struct DModel {
     const uint32_t* tface;
     // leaf clusters, 2 float4 per cluster: {lo.xyz, bound of |ab||ac| with
     // (n - 1) in its low 5 mantissa bits}, {hi.xyz, q}; cl_range = first cluster, count per
-    // node. Cluster c owns the primitive slots [16 c, 16 c + n) and the 128-B block clus[8 c ..]:
-    // its record (2 words), then (cnrm = clus + 2) 6 words of its screen normals
+    // node. Cluster c owns the primitive slots [16 c, 16 c + n) and the 256-B block clus[16 c ..]:
+    // its record (2 words), then (cnrm = clus + 2) 6 words of its screen normals, then 4 words
+    // of bounding spheres (one u32 per slot: centre u8 x 3, radius u8)
     // n = ab x ac as f16 integer multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
     // c1 = {ab.yz, ac.xy}, c2 = {ac.z, bits(leaf rank)}, cface = face index
     const float4_t* clus;

@@ -62,7 +62,7 @@ static bool box_check(V3 o, V3 inv, const float* b) {
     return !((tmin > tzmax) || (tzmin > tmax));
 }
 
-struct Stats { double rays = 0, active = 0, leaves = 0, crec = 0, cpass = 0, screen = 0, full = 0, nb_cull = 0; };
+struct Stats { double rays = 0, active = 0, leaves = 0, crec = 0, cpass = 0, screen = 0, full = 0, nb_cull = 0, sph = 0; };
 
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: cluster_sim OBJ [step] [cluster]\n"); return 2; }
@@ -225,6 +225,22 @@ int main(int argc, char** argv) {
                             S.full += 1;
                             if (dump && s == 0) pix[(size_t(y) * cm.width + x) * 5 + 3] += 1;
                             const float* v = &T.prim_vertices[9 * size_t(C.order[k])];
+                            {   // would a bounding-sphere line test (u8-quantized centre/radius) keep it?
+                                double cc[3], rr = 0;
+                                for (int q = 0; q < 3; ++q) cc[q] = (double(v[q]) + v[3 + q] + v[6 + q]) / 3.0;
+                                for (int j = 0; j < 3; ++j) {
+                                    double d2 = 0;
+                                    for (int q = 0; q < 3; ++q) d2 += (v[3 * j + q] - cc[q]) * (v[3 * j + q] - cc[q]);
+                                    rr = std::max(rr, std::sqrt(d2));
+                                }
+                                const double emax = std::max(ex, std::max(ey, ez));
+                                const double R = rr + 1.8 * emax / 255.0 + pad(det >= tau ? tau : kTol);
+                                const double w[3] = {cc[0] - eye.x, cc[1] - eye.y, cc[2] - eye.z};
+                                const double dd[3] = {d.x, d.y, d.z};
+                                const double cx = w[1] * dd[2] - w[2] * dd[1], cy = w[2] * dd[0] - w[0] * dd[2],
+                                             cz = w[0] * dd[1] - w[1] * dd[0];
+                                if (cx * cx + cy * cy + cz * cz <= R * R) S.sph += 1;
+                            }
                             const V3 a = mk(v[0], v[1], v[2]);
                             const float t = tri_hit(eye, d, a, sub(mk(v[3], v[4], v[5]), a), sub(mk(v[6], v[7], v[8]), a));
                             if (t > kTol && t < best) { best = t; improved = true; }
@@ -243,8 +259,8 @@ int main(int argc, char** argv) {
     for (int s = 0; s < NS; ++s) {
         const Stats& S = st[s];
         const double a = S.active;
-        std::printf("%-28s per active ray: leaves %.2f  cluster recs %.1f  boxes passed %.1f  normal-culled %.1f  screens %.1f  full tests %.1f\n",
-                    names[s], S.leaves / a, S.crec / a, S.cpass / a, S.nb_cull / a, S.screen / a, S.full / a);
+        std::printf("%-28s per active ray: leaves %.2f  cluster recs %.1f  boxes passed %.1f  normal-culled %.1f  screens %.1f  full tests %.1f  after sphere test %.2f\n",
+                    names[s], S.leaves / a, S.crec / a, S.cpass / a, S.nb_cull / a, S.screen / a, S.full / a, S.sph / a);
     }
     return 0;
 }
