@@ -438,6 +438,17 @@ int atr_octree_build(const atr_mesh* m, uint32_t max_faces, atr_octree** out) {
     return ATR_OK;
 }
 
+int atr_octree_build_device(const atr_mesh* m, uint32_t max_faces, int32_t device, atr_octree** out,
+                            float ms_out[2]) {
+    if (!m || !out || device < 0) return ATR_E_INVALID;
+    atr_octree* t = new (std::nothrow) atr_octree();
+    if (!t) return ATR_E_NOMEM;
+    const int rc = octree_build_device(m->m, max_faces, device, t->t, ms_out);
+    if (rc != ATR_OK) { delete t; return rc; }
+    *out = t;
+    return ATR_OK;
+}
+
 int atr_octree_from_nodes(int32_t nnodes, const float* bounds, const int32_t* children,
                           const uint32_t* leaf_first, const uint32_t* leaf_count, uint32_t nprims,
                           const float* prim_vertices, const uint32_t* prim_face, atr_octree** out) {

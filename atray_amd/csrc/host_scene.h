@@ -51,6 +51,7 @@ int parse_obj_text(const char* text, size_t len, HostMesh& m);
 void mesh_aabb(const HostMesh& m, float out[6]);
 void mesh_translate(HostMesh& m, float box[6], V3 c);
 int octree_build(const HostMesh& m, uint32_t max_faces, HostTree& T);
+int octree_build_device(const HostMesh& m, uint32_t max_faces, int device, HostTree& T, float* ms_out);  // build.hip
 int octree_finish(HostTree& T);
 void octree_stats(const HostTree& T, int64_t s[7]);
 void camera_set(atr_camera& cm, V3 eye, V3 facing, int32_t w, int32_t h, int32_t aa, uint32_t spp,

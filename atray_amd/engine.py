@@ -85,7 +85,7 @@ class atr_frame(C.Structure):
 # every symbol include/atray.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = [
     "atr_mesh_load_obj", "atr_mesh_parse_obj", "atr_mesh_from_arrays", "atr_mesh_free",
-    "atr_mesh_info", "atr_mesh_aabb", "atr_mesh_translate_to", "atr_octree_build",
+    "atr_mesh_info", "atr_mesh_aabb", "atr_mesh_translate_to", "atr_octree_build", "atr_octree_build_device",
     "atr_octree_from_nodes", "atr_octree_free", "atr_octree_export", "atr_octree_stats", "atr_camera_set",
     "atr_make_tiles", "atr_make_shard_tiles", "atr_create", "atr_destroy", "atr_version",
     "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
@@ -118,6 +118,7 @@ def lib():
         "atr_mesh_aabb": ([vp, C.c_float * 6], C.c_int),
         "atr_mesh_translate_to": ([vp, C.c_float * 6, atr_vec3], C.c_int),
         "atr_octree_build": ([vp, u32, P(vp)], C.c_int),
+        "atr_octree_build_device": ([vp, u32, i32, P(vp), vp], C.c_int),
         "atr_octree_from_nodes": ([i32, vp, vp, vp, vp, u32, vp, vp, P(vp)], C.c_int),
         "atr_octree_free": ([vp], None),
         "atr_octree_export": ([vp, vp, vp, vp, vp, vp, vp], C.c_int),
@@ -281,6 +282,18 @@ class Octree:
     def build(cls, mesh: Mesh, max_faces=300):
         h = C.c_void_p()
         check(lib().atr_octree_build(mesh.h, int(max_faces), C.byref(h)), "octree build")
+        return cls(h.value)
+
+    @classmethod
+    def build_device(cls, mesh: Mesh, max_faces=300, device=0, timings=None):
+        """f3: the same build on the GPU (build.hip), bit-identical to build(). `timings`, if a
+        dict, receives wall_ms (whole call) and device_ms (build kernels)."""
+        h = C.c_void_p()
+        ms = (C.c_float * 2)()
+        check(lib().atr_octree_build_device(mesh.h, int(max_faces), int(device), C.byref(h), ms),
+              "octree build (device)")
+        if timings is not None:
+            timings["wall_ms"], timings["device_ms"] = float(ms[0]), float(ms[1])
         return cls(h.value)
 
     @classmethod

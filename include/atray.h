@@ -71,6 +71,12 @@ int atr_octree_build(const atr_mesh* m, uint32_t max_faces, atr_octree** out);
 int atr_octree_from_nodes(int32_t nnodes, const float* node_bounds, const int32_t* node_children,
                           const uint32_t* leaf_first, const uint32_t* leaf_count, uint32_t nprims,
                           const float* prim_vertices, const uint32_t* prim_face, atr_octree** out);
+/* f3: the same build on GPU `device` (atray_amd/csrc/build.hip): level-synchronous
+   split sums and ordered vertex-in-box partitions as HIP kernels, nodes numbered in the
+   reference's LIFO order on the host. Result bit-identical to atr_octree_build. ms_out (may be
+   NULL): [0] wall time of the call incl. transfers, [1] device time of the build kernels. */
+int atr_octree_build_device(const atr_mesh* m, uint32_t max_faces, int32_t device, atr_octree** out,
+                            float ms_out[2]);
 void atr_octree_free(atr_octree* t);
 /* Copy the flattened tree out (any pointer may be NULL): 6 floats and children_start_position
    per node, leaf primitive range per node, 9 floats + face index per leaf primitive. */
