@@ -55,6 +55,14 @@ struct BlockSet {
     DevBuf dev_tiles;
     DevBuf dev_pix;  // pixel index per packed slot (wavefront schedule)
     int64_t packed_pixels = 0;
+    hipEvent_t ev = nullptr;  // recorded on the stream of every launch that reads this set
+    bool used = false;
+};
+
+// Device scratch freed on every exit path.
+struct DevTmp {
+    void* p = nullptr;
+    ~DevTmp() { if (p) (void)hipFree(p); }
 };
 
 // first_emit > 0: the pixels of tiles[0, first_emit) are left out (they belong to an earlier
@@ -133,6 +141,14 @@ int32_t qchunk() {
     static const int32_t v = std::max(1, env_int("ATR_QCHUNK", 16));
     return v;
 }
+// load_model_data's pool size (OBJ_loader.cpp:298: one chunk per pool thread): the host's
+// hardware threads, at most 16 (ATR_PARSE_THREADS overrides).
+int32_t default_parse_threads() {
+    const int32_t e = env_int("ATR_PARSE_THREADS", 0);
+    if (e > 0) return e;
+    const unsigned hw = std::thread::hardware_concurrency();
+    return int32_t(std::max(1u, std::min(16u, hw)));
+}
 constexpr int kSchedPersist = 8;
 constexpr int kQueueSlots = 32;             // queue-head sets in flight (ring)
 constexpr size_t kQueueBytes = 8 * 32 * 4;  // 8 heads, 128 B apart
@@ -176,6 +192,9 @@ struct atr_ctx {
     std::vector<DevBuf> prog_blocks;
     std::vector<hipEvent_t> prog_ev;
     std::vector<int32_t> prog_end;
+    // last launch per stream: everything this context has in flight (scene frees, workspace
+    // regrowth and progressive group buffers wait for all of them)
+    std::vector<std::pair<hipStream_t, hipEvent_t>> stream_ev;
 };
 
 namespace {
@@ -184,17 +203,48 @@ int dev_upload(atr_ctx* c, const void* src, size_t bytes, void** out) {
     DevBuf b;
     b.n = bytes ? bytes : 16;
     HIPCHK(hipMalloc(&b.p, b.n));
-    if (bytes) HIPCHK(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    if (bytes) {
+        const hipError_t e = hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(b.p);
+            return -(1000 + int(e));
+        }
+    }
     c->scene_bufs.push_back(b);
     c->scene_bytes += int64_t(b.n);
     *out = b.p;
     return ATR_OK;
 }
 
+// Record that a launch on stream s is in flight (one reusable event per stream).
+hipError_t note_launch(atr_ctx* c, hipStream_t s, BlockSet* bs) {
+    hipError_t e = hipSuccess;
+    if (bs) {
+        if (!bs->ev && (e = hipEventCreateWithFlags(&bs->ev, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventRecord(bs->ev, s)) != hipSuccess) return e;
+        bs->used = true;
+    }
+    for (auto& se : c->stream_ev)
+        if (se.first == s) return hipEventRecord(se.second, s);
+    hipEvent_t ev = nullptr;
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    c->stream_ev.emplace_back(s, ev);
+    return hipEventRecord(ev, s);
+}
+
+// Wait for every launch of this context still in flight, on any stream.
+hipError_t wait_all(atr_ctx* c) {
+    for (auto& se : c->stream_ev) {
+        const hipError_t e = hipEventSynchronize(se.second);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 // Carve the wavefront workspace for n path slots and a tree of `nodes` nodes.
 int wf_reserve(atr_ctx* c, int64_t n, int64_t nodes) {
     if (n <= c->wf_n && nodes <= c->wf_nodes && c->wf_mem.p) return ATR_OK;
-    if (c->have_render) HIPCHK(hipEventSynchronize(c->ev_done));
+    HIPCHK(wait_all(c));
     if (c->wf_mem.p) HIPCHK(hipFree(c->wf_mem.p));
     c->wf_mem = DevBuf();
     n = std::max<int64_t>(n, c->wf_n);
@@ -275,8 +325,12 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     }
     BlockSet& b = c->blocks[lru];
     c->block_use[lru] = ++c->use_clock;
-    // the slot may still be read by an in-flight kernel of an earlier render
-    if (c->have_render) (void)hipEventSynchronize(c->ev_done);
+    // the slot may still be read by an in-flight kernel of an earlier render, on any stream
+    if (b.used) {
+        const hipError_t e = hipEventSynchronize(b.ev);
+        if (e != hipSuccess) { rc = -(1000 + int(e)); return nullptr; }
+        b.used = false;
+    }
     b.tiles.assign(tiles, tiles + ntiles);
     b.width = W;
     b.height = H;
@@ -367,27 +421,41 @@ extern "C" {
 const char* atr_version(void) { return "atray-mi355x 0.1 (gfx950)"; }
 
 // ------------------------------------------------------------------ host prerequisites
-int atr_mesh_parse_obj(const char* text, size_t len, atr_mesh** out) {
-    if (!text || !out) return ATR_E_INVALID;
+int atr_mesh_parse_obj_threaded(const char* text, size_t len, int32_t threads, atr_mesh** out) {
+    if (!text || !out || threads < 0) return ATR_E_INVALID;
+    if (threads == 0) threads = default_parse_threads();
     atr_mesh* m = new (std::nothrow) atr_mesh();
     if (!m) return ATR_E_NOMEM;
-    const int rc = parse_obj_text(text, len, m->m);
+    const int rc = parse_obj_text(text, len, m->m, threads);
     if (rc != ATR_OK) { delete m; return rc; }
     *out = m;
     return ATR_OK;
 }
 
-int atr_mesh_load_obj(const char* path, atr_mesh** out) {
-    if (!path || !out) return ATR_E_INVALID;
+int atr_mesh_parse_obj(const char* text, size_t len, atr_mesh** out) {
+    return atr_mesh_parse_obj_threaded(text, len, 1, out);
+}
+
+int atr_mesh_load_obj_threaded(const char* path, int32_t threads, atr_mesh** out) {
+    if (!path || !out || threads < 0) return ATR_E_INVALID;
     FILE* f = std::fopen(path, "rb");
     if (!f) return ATR_E_IO;
     std::string buf;
+    if (std::fseek(f, 0, SEEK_END) == 0) {
+        const long sz = std::ftell(f);
+        if (sz > 0) buf.reserve(size_t(sz));
+        std::rewind(f);
+    }
     char tmp[1 << 16];
     size_t n;
     while ((n = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.append(tmp, n);
+    const bool bad = std::ferror(f) != 0;
     std::fclose(f);
-    return atr_mesh_parse_obj(buf.data(), buf.size(), out);
+    if (bad) return ATR_E_IO;
+    return atr_mesh_parse_obj_threaded(buf.data(), buf.size(), threads, out);
 }
+
+int atr_mesh_load_obj(const char* path, atr_mesh** out) { return atr_mesh_load_obj_threaded(path, 0, out); }
 
 int atr_mesh_from_arrays(const float* vertices, uint32_t nvertices, const int32_t* face_vertices,
                          uint32_t nfaces, const float* normals, uint32_t nnormals,
@@ -413,6 +481,23 @@ int atr_mesh_info(const atr_mesh* m, uint32_t* nv, uint32_t* nn, uint32_t* nf) {
     if (nv) *nv = uint32_t(m->m.vertices.size());
     if (nn) *nn = uint32_t(m->m.normals.size());
     if (nf) *nf = uint32_t(m->m.nfaces());
+    return ATR_OK;
+}
+
+int atr_mesh_export(const atr_mesh* m, float* vertices, float* normals, float* texcoords, uint32_t* ntexcoords,
+                    int32_t* face_v, int32_t* face_t, int32_t* face_n) {
+    if (!m) return ATR_E_INVALID;
+    auto put = [](float* dst, const std::vector<V3>& src) {
+        if (!dst) return;
+        for (size_t i = 0; i < src.size(); ++i) { dst[3 * i] = src[i].x; dst[3 * i + 1] = src[i].y; dst[3 * i + 2] = src[i].z; }
+    };
+    put(vertices, m->m.vertices);
+    put(normals, m->m.normals);
+    put(texcoords, m->m.texcoords);
+    if (ntexcoords) *ntexcoords = uint32_t(m->m.texcoords.size());
+    if (face_v) std::memcpy(face_v, m->m.face_v.data(), m->m.face_v.size() * sizeof(int32_t));
+    if (face_t) std::memcpy(face_t, m->m.face_t.data(), m->m.face_t.size() * sizeof(int32_t));
+    if (face_n) std::memcpy(face_n, m->m.face_n.data(), m->m.face_n.size() * sizeof(int32_t));
     return ATR_OK;
 }
 
@@ -580,16 +665,23 @@ int atr_create(int device, atr_ctx** out) {
     atr_ctx* c = new (std::nothrow) atr_ctx();
     if (!c) return ATR_E_NOMEM;
     c->device = device;
-    HIPCHK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&c->ev_start));
-    HIPCHK(hipEventCreate(&c->ev_stop));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&c->d_error, 16));
-    HIPCHK(hipMemset(c->d_error, 0, 16));
-    HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
-    HIPCHK(hipMalloc(&c->qring, kQueueSlots * kQueueBytes));
-    HIPCHK(hipMemset(c->qring, 0, kQueueSlots * kQueueBytes));
-    for (hipEvent_t& e : c->qev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const int rc = [&]() -> int {  // any failure below releases what was created (atr_destroy)
+        HIPCHK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&c->ev_start));
+        HIPCHK(hipEventCreate(&c->ev_stop));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+        HIPCHK(hipMalloc(&c->d_error, 16));
+        HIPCHK(hipMemset(c->d_error, 0, 16));
+        HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
+        HIPCHK(hipMalloc(&c->qring, kQueueSlots * kQueueBytes));
+        HIPCHK(hipMemset(c->qring, 0, kQueueSlots * kQueueBytes));
+        for (hipEvent_t& e : c->qev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        return ATR_OK;
+    }();
+    if (rc != ATR_OK) {
+        atr_destroy(c);
+        return rc;
+    }
     *out = c;
     return ATR_OK;
 }
@@ -603,7 +695,9 @@ int atr_destroy(atr_ctx* c) {
         if (b.dev.p) (void)hipFree(b.dev.p);
         if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
         if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
+        if (b.ev) (void)hipEventDestroy(b.ev);
     }
+    for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
     if (c->wf_mem.p) (void)hipFree(c->wf_mem.p);
     if (c->wf_pinned) (void)hipHostFree(c->wf_pinned);
     if (c->d_error) (void)hipFree(c->d_error);
@@ -614,10 +708,10 @@ int atr_destroy(atr_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->qev)
         if (e) (void)hipEventDestroy(e);
-    (void)hipEventDestroy(c->ev_start);
-    (void)hipEventDestroy(c->ev_stop);
-    (void)hipEventDestroy(c->ev_done);
-    (void)hipStreamDestroy(c->own_stream);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return ATR_OK;
 }
@@ -628,6 +722,10 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
     if (!c || !mats || nmats <= 0 || nmats > kMaxMaterials || nmodels < 0 || nmodels > kMaxModels ||
         (nmodels && !models) || nspheres < 0 || nplanes < 0 || (nspheres && !spheres) || (nplanes && !planes))
         return ATR_E_INVALID;
+    for (int32_t i = 0; i < nspheres; ++i)  // shading indexes mats[material] on the device
+        if (spheres[i].material < 0 || spheres[i].material >= nmats) return ATR_E_INVALID;
+    for (int32_t i = 0; i < nplanes; ++i)
+        if (planes[i].material < 0 || planes[i].material >= nmats) return ATR_E_INVALID;
     for (int32_t i = 0; i < nmodels; ++i) {
         const atr_model& md = models[i];
         if (!md.mesh || md.material < 0 || md.material >= nmats) return ATR_E_INVALID;
@@ -637,7 +735,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
         }
     }
     HIPCHK(hipSetDevice(c->device));
-    if (c->have_render) HIPCHK(hipEventSynchronize(c->ev_done));
+    HIPCHK(wait_all(c));  // kernels on any stream may still read the old scene
     free_scene(c);
     DScene S;
     std::memset(&S, 0, sizeof(S));
@@ -997,6 +1095,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
             HIPCHK(atr_wf_render(W, c->nmodels, c->model_nodes.data(), c->model_tree.data(), c->wf_pinned, s));
         HIPCHK(hipEventRecord(c->ev_stop, s));
         HIPCHK(hipEventRecord(c->ev_done, s));
+        HIPCHK(note_launch(c, s, bs));
         c->have_render = true;
         c->last_stream = s;
         c->last_ntiles = ntiles;
@@ -1024,18 +1123,30 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     HIPCHK(launch_render(c, P, wave, s));
     HIPCHK(hipEventRecord(c->ev_stop, s));
     HIPCHK(hipEventRecord(c->ev_done, s));
+    HIPCHK(note_launch(c, s, bs));
     c->have_render = true;
     c->last_stream = s;
     c->last_ntiles = ntiles;
     return ATR_OK;
 }
 
-int atr_render_start_frames(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                            const atr_frame* fr, int32_t nframes, int64_t frame_stride, uint64_t seed, void* stream,
-                            int32_t variant) {
-    if (!c || !cam || !fr || !fr->framebuffer || ntiles < 0 || (ntiles && !tiles) || nframes < 1 || nframes > 64)
+namespace {
+// Frames in flight in one launch (atr_render_start_frames / _cameras): ncams == 1 -> every frame
+// renders cams[0]; ncams == nframes -> frame f renders cams[f].
+int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_tile* tiles, int32_t ntiles,
+                 const atr_frame* fr, int32_t nframes, int64_t frame_stride, uint64_t seed, void* stream,
+                 int32_t variant) {
+    if (!c || !cams || !fr || !fr->framebuffer || ntiles < 0 || (ntiles && !tiles) || nframes < 1 || nframes > 64)
         return ATR_E_INVALID;
+    if (ncams != 1 && (ncams != nframes || nframes > kMaxFrameCams)) return ATR_E_INVALID;
+    const atr_camera* cam = cams;
     if (cam->width <= 0 || cam->height <= 0 || cam->width > (1 << 16) || cam->height > (1 << 16)) return ATR_E_INVALID;
+    for (int32_t f = 1; f < ncams; ++f) {  // one block list and one kernel specialization per launch
+        const atr_camera& q = cams[f];
+        if (q.width != cam->width || q.height != cam->height || q.samples_per_pixel != cam->samples_per_pixel ||
+            q.bounce_limit != cam->bounce_limit || q.anti_aliasing != cam->anti_aliasing)
+            return ATR_E_INVALID;
+    }
     if (fr->layout != ATR_LAYOUT_IMAGE && fr->layout != ATR_LAYOUT_PACKED) return ATR_E_INVALID;
     if (variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
@@ -1070,11 +1181,16 @@ int atr_render_start_frames(atr_ctx* c, const atr_camera* cam, const atr_tile* t
         P.nblocks = nb * nframes;
         P.frame_blocks = nb;
         P.frame_stride = frame_stride;
+        if (ncams > 1) {
+            P.nfcam = ncams;
+            for (int32_t f = 0; f < ncams; ++f) P.fcam[f] = cams[f];
+        }
         HIPCHK(launch_render(c, P, sched, s));
     } else {  // persistent lanes take pixels from a queue: one launch per frame
         P.nblocks = nb;
         for (int32_t f = 0; f < nframes; ++f) {
             const size_t o = size_t(f) * size_t(frame_stride);
+            P.cam = cams[ncams > 1 ? f : 0];
             P.framebuffer = fr->framebuffer + o;
             P.hit_face = fr->hit_face ? fr->hit_face + o : nullptr;
             P.hit_t = fr->hit_t ? fr->hit_t + o : nullptr;
@@ -1085,10 +1201,24 @@ int atr_render_start_frames(atr_ctx* c, const atr_camera* cam, const atr_tile* t
     }
     HIPCHK(hipEventRecord(c->ev_stop, s));
     HIPCHK(hipEventRecord(c->ev_done, s));
+    HIPCHK(note_launch(c, s, bs));
     c->have_render = true;
     c->last_stream = s;
     c->last_ntiles = ntiles;
     return ATR_OK;
+}
+}  // namespace
+
+int atr_render_start_frames(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                            const atr_frame* fr, int32_t nframes, int64_t frame_stride, uint64_t seed, void* stream,
+                            int32_t variant) {
+    return start_frames(c, cam, 1, tiles, ntiles, fr, nframes, frame_stride, seed, stream, variant);
+}
+
+int atr_render_start_cameras(atr_ctx* c, const atr_camera* cams, int32_t nframes, const atr_tile* tiles,
+                             int32_t ntiles, const atr_frame* fr, int64_t frame_stride, uint64_t seed, void* stream,
+                             int32_t variant) {
+    return start_frames(c, cams, nframes, tiles, ntiles, fr, nframes, frame_stride, seed, stream, variant);
 }
 
 int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
@@ -1102,10 +1232,10 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     const size_t nb = bs->host.size();
     *nblocks = int64_t(nb);
     if (!out || cap < int64_t(3 * nb)) return ATR_OK;  // size query
-    void* fb = nullptr;
-    void* tr = nullptr;
-    HIPCHK(hipMalloc(&fb, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
-    HIPCHK(hipMalloc(&tr, std::max<size_t>(1, 3 * nb) * sizeof(unsigned long long)));
+    DevTmp fb;
+    DevTmp tr;
+    HIPCHK(hipMalloc(&fb.p, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
+    HIPCHK(hipMalloc(&tr.p, std::max<size_t>(1, 3 * nb) * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1114,16 +1244,14 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.blocks = static_cast<const DBlock*>(bs->dev.p);
     P.nblocks = int32_t(nb);
     P.layout = ATR_LAYOUT_PACKED;
-    P.framebuffer = static_cast<uint32_t*>(fb);
+    P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
-    P.wave_trace = static_cast<unsigned long long*>(tr);
+    P.wave_trace = static_cast<unsigned long long*>(tr.p);
     P.xcd_chunk = xcd_chunk();
     const int ts = sched_of(variant);  // per-cell trace: 8x8-cell schedules only
     HIPCHK(atr_launch_render(P, ts == kSchedPersist ? 4 : ts, nullptr));
     HIPCHK(hipDeviceSynchronize());
-    if (nb) HIPCHK(hipMemcpy(out, tr, 3 * nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    HIPCHK(hipFree(fb));
-    HIPCHK(hipFree(tr));
+    if (nb) HIPCHK(hipMemcpy(out, tr.p, 3 * nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;
 }
 
@@ -1135,11 +1263,11 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     int rc = ATR_OK;
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
-    void* fb = nullptr;
-    void* ctr = nullptr;
-    HIPCHK(hipMalloc(&fb, size_t(cam->width) * size_t(cam->height) * 4));
-    HIPCHK(hipMalloc(&ctr, 10 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(ctr, 0, 10 * sizeof(unsigned long long)));
+    DevTmp fb;
+    DevTmp ctr;
+    HIPCHK(hipMalloc(&fb.p, size_t(cam->width) * size_t(cam->height) * 4));
+    HIPCHK(hipMalloc(&ctr.p, 10 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctr.p, 0, 10 * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1148,17 +1276,15 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.blocks = static_cast<const DBlock*>(bs->dev.p);
     P.nblocks = int32_t(bs->host.size());
     P.layout = ATR_LAYOUT_IMAGE;
-    P.framebuffer = static_cast<uint32_t*>(fb);
+    P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
-    P.counters = static_cast<unsigned long long*>(ctr);
+    P.counters = static_cast<unsigned long long*>(ctr.p);
     const int sc = auto_sched(variant, *cam);
     HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
     unsigned long long h[10];
-    HIPCHK(hipMemcpy(h, ctr, sizeof(h), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h, ctr.p, sizeof(h), hipMemcpyDeviceToHost));
     for (int k = 0; k < 10; ++k) out[k] = int64_t(h[k]);
-    HIPCHK(hipFree(fb));
-    HIPCHK(hipFree(ctr));
     return ATR_OK;
 }
 
@@ -1171,10 +1297,10 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
     const size_t nb = bs->host.size();
-    void* fb = nullptr;
-    void* cost = nullptr;
-    HIPCHK(hipMalloc(&fb, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
-    HIPCHK(hipMalloc(&cost, std::max<size_t>(1, nb) * sizeof(unsigned long long)));
+    DevTmp fb;
+    DevTmp cost;
+    HIPCHK(hipMalloc(&fb.p, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
+    HIPCHK(hipMalloc(&cost.p, std::max<size_t>(1, nb) * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1183,16 +1309,14 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.blocks = static_cast<const DBlock*>(bs->dev.p);
     P.nblocks = int32_t(nb);
     P.layout = ATR_LAYOUT_PACKED;
-    P.framebuffer = static_cast<uint32_t*>(fb);
+    P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
-    P.block_cost = static_cast<unsigned long long*>(cost);
+    P.block_cost = static_cast<unsigned long long*>(cost.p);
     P.xcd_chunk = xcd_chunk();
     HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_CLUSTER), nullptr));  // per-cell clocks
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
-    if (nb) HIPCHK(hipMemcpy(h.data(), cost, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    HIPCHK(hipFree(fb));
-    HIPCHK(hipFree(cost));
+    if (nb) HIPCHK(hipMemcpy(h.data(), cost.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     // a block (one 8x8 cell of the image grid) belongs to the first tile (list order) that
     // overlaps it: paint cell owners in list order, first writer wins
     const int32_t cw = (cam->width + 7) / 8, chh = (cam->height + 7) / 8;
@@ -1226,7 +1350,7 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (c->have_render) HIPCHK(hipEventSynchronize(c->ev_done));  // group buffers are reused
+    HIPCHK(wait_all(c));  // group buffers are reused
     const int32_t ngroups = (ntiles + tiles_per_launch - 1) / tiles_per_launch;
     while (int32_t(c->prog_ev.size()) < ngroups) {
         hipEvent_t e;
@@ -1273,6 +1397,7 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
     }
     HIPCHK(hipEventRecord(c->ev_stop, s));
     HIPCHK(hipEventRecord(c->ev_done, s));
+    HIPCHK(note_launch(c, s, nullptr));
     c->have_render = true;
     c->prog_active = true;
     c->last_stream = s;
@@ -1336,6 +1461,7 @@ int atr_unpack(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width,
     if (!bs) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
     HIPCHK(atr_launch_unpack(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed, image, s));
+    HIPCHK(note_launch(c, s, bs));
     return ATR_OK;
 }
 

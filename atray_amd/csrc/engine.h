@@ -3,6 +3,7 @@
 // precomputation and the kernels evaluate the same expressions in the same order
 // (reference op order: PL/PL_math.h:106-123,416-422). Built with -ffp-contract=off.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include "../../include/atray.h"
@@ -31,6 +32,7 @@ constexpr float kInvU32Max = 2.328306437e-10F;    // PL_base_defs.h:75
 constexpr float kTol = 0.0001f;                   // ray.h:5
 constexpr int kMaskLevels = 16;                   // traversal mask-stack depth (8 bits/level)
 constexpr int kMaxMaterials = 32;
+constexpr int kMaxFrameCams = 16;  // distinct cameras per multi-frame launch (kernel argument)
 constexpr int kMaxModels = 8;
 constexpr int kMaxClusterSize = 16;  // primitive slots per leaf cluster (ATR_CLUSTER_SIZE <= this)
 constexpr int kClusterBlock = 16;    // 16-B words per cluster block: record (2), screen normals (6),
@@ -183,6 +185,8 @@ struct RenderParams {
     int32_t qchunk;     // PERSIST: 8x8 cells per queue chunk
     int32_t frame_blocks;  // > 0: nblocks = frames x frame_blocks, one launch renders every frame
     int64_t frame_stride;  // output elements between consecutive frames (rgb: 3 x this)
+    int32_t nfcam;         // > 0: frame f renders with fcam[f] instead of cam (same size/spp/bounces)
+    atr_camera fcam[kMaxFrameCams];
 };
 
 }  // namespace atr

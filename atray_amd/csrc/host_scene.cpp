@@ -16,124 +16,7 @@
 
 using namespace atr;
 
-namespace {
-
-// ------------------------------------------------------------------ text parsing
-// A cursor over NUL-free OBJ text that always ends in '\n' (OBJ_loader.cpp:330-331 appends one).
-struct Cursor {
-    const char* p;
-    bool at(char c) const { return *p == c; }
-    void skip_blanks() { while (*p == ' ' || *p == '\t' || *p == '\r') ++p; }  // parser.h:4-35
-    void to_next_line() { while (*p != '\n') ++p; ++p; }
-    static bool digit(char c) { return c >= '0' && c <= '9'; }
-
-    // parse_int (parser.h:38-65); int32 overflow wraps (the reference's is UB)
-    int32_t integer() {
-        skip_blanks();
-        uint32_t sgn = 1u;
-        if (*p == '+') ++p;
-        else if (*p == '-') { sgn = 0xFFFFFFFFu; ++p; }
-        uint32_t v = 0;
-        while (digit(*p)) v = v * 10u + uint32_t(*p++ - '0');
-        return int32_t(v * sgn);
-    }
-
-    // parse_f64 (parser.h:113-191): integer mantissa of all digits, one f64 multiply by the
-    // power-of-ten table entry for (exponent - fraction digits), table range 1e-28..1e19.
-    double real() {
-        static const double kPow10[48] = {
-            1.0e-28, 1.0e-27, 1.0e-26, 1.0e-25, 1.0e-24, 1.0e-23, 1.0e-22, 1.0e-21, 1.0e-20, 1.0e-19,
-            1.0e-18, 1.0e-17, 1.0e-16, 1.0e-15, 1.0e-14, 1.0e-13, 1.0e-12, 1.0e-11, 1.0e-10, 1.0e-9,
-            1.0e-8,  1.0e-7,  1.0e-6,  1.0e-5,  1.0e-4,  1.0e-3,  1.0e-2,  1.0e-1,  1.0e0,   1.0e1,
-            1.0e2,   1.0e3,   1.0e4,   1.0e5,   1.0e6,   1.0e7,   1.0e8,   1.0e9,   1.0e10,  1.0e11,
-            1.0e12,  1.0e13,  1.0e14,  1.0e15,  1.0e16,  1.0e17,  1.0e18,  1.0e19};
-        skip_blanks();
-        double sgn = 1.0;
-        if (*p == '+') ++p;
-        else if (*p == '-') { sgn = -1.0; ++p; }
-        uint64_t mant = 0;
-        while (digit(*p)) mant = mant * 10u + uint64_t(*p++ - '0');
-        if (*p == '.') ++p;
-        uint64_t frac = 0;
-        int ndig = 0;
-        while (digit(*p)) { frac = frac * 10u + uint64_t(*p++ - '0'); ++ndig; }
-        uint64_t scale10 = 1;
-        for (int i = 0; i < (ndig > 19 ? 19 : ndig); ++i) scale10 *= 10u;
-        mant = mant * scale10 + frac;
-        int e = 0;
-        if (*p == 'e' || *p == 'E') {
-            ++p;
-            int es = 1;
-            if (*p == '+') ++p;
-            else if (*p == '-') { es = -1; ++p; }
-            while (digit(*p)) e = 10 * e + (*p++ - '0');
-            e *= es;
-        }
-        e -= ndig;
-        double v = double(mant) * sgn;
-        if (e < -28 || e > 19) e = 0;
-        return v * kPow10[e + 28];
-    }
-    V3 vec3() {  // parse_vec3f (parser.h:194-205)
-        float x = float(real());
-        float y = float(real());
-        float z = float(real());
-        return mk(x, y, z);
-    }
-};
-
-}  // namespace
-
-// ------------------------------------------------------------------ mesh
-int atr::parse_obj_text(const char* text, size_t len, HostMesh& m) {
-    std::string buf(text, len);
-    buf.push_back('\n');
-    for (char& c : buf)
-        if (c == '\0') c = ' ';  // a NUL in the file would end the reference's line scan oddly
-    const char* end = buf.data() + buf.size();
-    Cursor cur{buf.data()};
-    m = HostMesh();
-    while (cur.p < end) {
-        if (cur.at('v')) {  // OBJ_loader.cpp:54-80
-            ++cur.p;
-            if (cur.at(' ')) m.vertices.push_back(cur.vec3());
-            else if (cur.at('t')) { ++cur.p; m.texcoords.push_back(cur.vec3()); }
-            else if (cur.at('n')) { ++cur.p; m.normals.push_back(cur.vec3()); }
-        } else if (cur.at('f')) {  // OBJ_loader.cpp:81-149: first three index groups only
-            ++cur.p;
-            int32_t v[3] = {0, 0, 0}, t[3] = {0, 0, 0}, n[3] = {0, 0, 0};
-            for (int k = 0; k < 3; ++k) {
-                v[k] = cur.integer();
-                if (cur.at('/')) {
-                    ++cur.p;
-                    if (cur.at('/')) { ++cur.p; n[k] = cur.integer(); }
-                    else {
-                        t[k] = cur.integer();
-                        if (cur.at('/')) { ++cur.p; n[k] = cur.integer(); }
-                    }
-                }
-            }
-            for (int k = 0; k < 3; ++k) {
-                m.face_v.push_back(v[k]);
-                m.face_t.push_back(t[k]);
-                m.face_n.push_back(n[k]);
-            }
-        }
-        cur.to_next_line();
-    }
-    // prep_model_data (OBJ_loader.cpp:229-267): relative indices, then drop the +1 offset
-    const int32_t nv = int32_t(m.vertices.size()), nn = int32_t(m.normals.size()),
-                  nt = int32_t(m.texcoords.size());
-    for (size_t i = 0; i < m.face_v.size(); ++i) {
-        if (m.face_t[i] < 0) m.face_t[i] += nt + 1;
-        if (m.face_n[i] < 0) m.face_n[i] += nn + 1;
-        if (m.face_v[i] < 0) m.face_v[i] += nv + 1;
-        m.face_t[i] -= 1;
-        m.face_v[i] -= 1;
-        m.face_n[i] -= 1;
-    }
-    return ATR_OK;
-}
+// OBJ text parsing (load_model_data, parse_f64): obj_parse.cpp
 
 void atr::mesh_aabb(const HostMesh& m, float out[6]) {  // get_AABB (model.h:41-61)
     float lo[3] = {kMaxFloat, kMaxFloat, kMaxFloat}, hi[3] = {-kMaxFloat, -kMaxFloat, -kMaxFloat};

@@ -47,7 +47,9 @@ int leaf_clusters(const HostTree& T, int size, LeafClusters& C);
 // the leaf's rank in the static discovery order (-1 for inner nodes): leaf ids on the device.
 int inner_table(const HostTree& T, std::vector<float4_t>& out, std::vector<int32_t>& leaf_rank);
 
-int parse_obj_text(const char* text, size_t len, HostMesh& m);
+// load_model_data (OBJ_loader.cpp:278-360) on `threads` newline-aligned chunks (obj_parse.cpp);
+// the result does not depend on `threads`.
+int parse_obj_text(const char* text, size_t len, HostMesh& m, int threads = 1);
 void mesh_aabb(const HostMesh& m, float out[6]);
 void mesh_translate(HostMesh& m, float box[6], V3 c);
 int octree_build(const HostMesh& m, uint32_t max_faces, HostTree& T);

@@ -511,7 +511,9 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
     const uint64_t clk0 = P.block_cost ? clock64() : 0;
     const uint64_t rt0 = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0;
-    const atr_camera& cm = P.cam;
+    // per-frame cameras (atr_render_start_cameras): fidx is wave-uniform, so the camera comes from
+    // the kernel argument with scalar loads
+    const atr_camera& cm = P.nfcam > 0 ? P.fcam[__builtin_amdgcn_readfirstlane(fidx)] : P.cam;
     const DScene* S = P.scene;
     int err = 0;
     Ctr ct;

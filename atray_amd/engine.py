@@ -93,6 +93,8 @@ EXPORTS = [
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
+    "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
+    "atr_mesh_export",
 ]
 
 _lib = None
@@ -112,9 +114,12 @@ def lib():
     sig = {
         "atr_mesh_load_obj": ([C.c_char_p, P(vp)], C.c_int),
         "atr_mesh_parse_obj": ([C.c_char_p, C.c_size_t, P(vp)], C.c_int),
+        "atr_mesh_load_obj_threaded": ([C.c_char_p, i32, P(vp)], C.c_int),
+        "atr_mesh_parse_obj_threaded": ([C.c_char_p, C.c_size_t, i32, P(vp)], C.c_int),
         "atr_mesh_from_arrays": ([vp, u32, vp, u32, vp, u32, vp, P(vp)], C.c_int),
         "atr_mesh_free": ([vp], None),
         "atr_mesh_info": ([vp, P(u32), P(u32), P(u32)], C.c_int),
+        "atr_mesh_export": ([vp, vp, vp, vp, P(u32), vp, vp, vp], C.c_int),
         "atr_mesh_aabb": ([vp, C.c_float * 6], C.c_int),
         "atr_mesh_translate_to": ([vp, C.c_float * 6, atr_vec3], C.c_int),
         "atr_octree_build": ([vp, u32, P(vp)], C.c_int),
@@ -147,6 +152,7 @@ def lib():
         "atr_write_bmp": ([vp, i32, i32, C.c_char_p, C.c_char_p, i32], C.c_int),
         "atr_render_start_frames": ([vp, P(atr_camera), vp, i32, P(atr_frame), i32, i64, C.c_uint64, vp, i32],
                                     C.c_int),
+        "atr_render_start_cameras": ([vp, vp, i32, vp, i32, P(atr_frame), i64, C.c_uint64, vp, i32], C.c_int),
         "atr_last_kernel_ms": ([vp, P(C.c_float)], C.c_int),
         "atr_device_alloc": ([vp, C.c_size_t, P(vp)], C.c_int),
         "atr_device_free": ([vp, vp], C.c_int),
@@ -239,17 +245,35 @@ class Mesh:
         self.h = C.c_void_p(handle)
 
     @classmethod
-    def load_obj(cls, path):
+    def load_obj(cls, path, threads=None):
+        """load_model_data; threads None = the library default (host threads, at most 16)."""
         h = C.c_void_p()
-        check(lib().atr_mesh_load_obj(os.fsencode(path), C.byref(h)), f"load {path}")
+        if threads is None:
+            check(lib().atr_mesh_load_obj(os.fsencode(path), C.byref(h)), f"load {path}")
+        else:
+            check(lib().atr_mesh_load_obj_threaded(os.fsencode(path), int(threads), C.byref(h)), f"load {path}")
         return cls(h.value)
 
     @classmethod
-    def parse_obj(cls, text):
+    def parse_obj(cls, text, threads=1):
         b = text.encode() if isinstance(text, str) else bytes(text)
         h = C.c_void_p()
-        check(lib().atr_mesh_parse_obj(b, len(b), C.byref(h)), "parse obj")
+        check(lib().atr_mesh_parse_obj_threaded(b, len(b), int(threads), C.byref(h)), "parse obj")
         return cls(h.value)
+
+    def arrays(self):
+        """ModelData copied out: vertices, normals, texcoords (n, 3) f32; face vertex, texcoord
+        and normal indices (nfaces, 3) i32, 0-based (-1 = absent)."""
+        nv, nn, nf = self.info()
+        nt = C.c_uint32()
+        check(lib().atr_mesh_export(self.h, None, None, None, C.byref(nt), None, None, None), "mesh export")
+        V = np.zeros((max(nv, 1), 3), np.float32)
+        N = np.zeros((max(nn, 1), 3), np.float32)
+        T = np.zeros((max(nt.value, 1), 3), np.float32)
+        FV, FT, FN = (np.zeros((max(nf, 1), 3), np.int32) for _ in range(3))
+        check(lib().atr_mesh_export(self.h, V.ctypes.data, N.ctypes.data, T.ctypes.data, C.byref(nt),
+                                    FV.ctypes.data, FT.ctypes.data, FN.ctypes.data), "mesh export")
+        return V[:nv], N[:nn], T[:nt.value], FV[:nf], FT[:nf], FN[:nf]
 
     def info(self):
         nv, nn, nf = C.c_uint32(), C.c_uint32(), C.c_uint32()
@@ -405,6 +429,16 @@ class Engine:
                                             int(nframes), int(frame_stride), C.c_uint64(seed & (2**64 - 1)),
                                             C.c_void_p(stream) if stream else None, int(variant)),
               "render start frames")
+
+    def render_start_cameras(self, cams, tiles, frame: atr_frame, frame_stride, seed, stream=None,
+                             variant=ATR_KERNEL_AUTO):
+        """len(cams) frames (at most 16) in one launch, frame f from cams[f]; outputs frame_stride apart."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        ca = (atr_camera * len(cams))(*cams)
+        check(lib().atr_render_start_cameras(self.h, C.cast(ca, C.c_void_p), len(cams), C.cast(arr, C.c_void_p), n,
+                                             C.byref(frame), int(frame_stride), C.c_uint64(seed & (2**64 - 1)),
+                                             C.c_void_p(stream) if stream else None, int(variant)),
+              "render start cameras")
 
     def counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
         arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)

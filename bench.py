@@ -1,28 +1,42 @@
-"""Benchmark: Mrays/s of the render path on Dragon 1920x1080 (BASELINE.json metric, config 3).
+"""Benchmark: Mrays/s of the render path on Dragon 1920x1080 (BASELINE.json metric, config c3).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--variant auto|lane|wave]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c5|...] [--variant auto|cl|ps|lane|...]
 
-One step = one frame of the config rendered by all ranks: each rank traces its 64x64 shard tiles
-into a packed buffer; for N > 1 the packed buffers are gathered to rank 0 over RCCL
-(torch.distributed "nccl", async, double-buffered: frame k's gather overlaps frame k+1's render)
-and scattered into the frame there. Tiles are dealt longest-first by cost measured in one
-calibration render on rank 0 (--plan cost, default; --plan rr = round-robin). The scene
-(OBJ load, octree build, upload) and the plan are prepared before timing; inputs are resident
-in HBM when the timed region starts. value = traced rays of all ranks / max-over-ranks wall
-time. ATR_DIST_BACKEND=gloo rehearses N ranks on one GPU (host-staged gather).
+One step = one frame rendered by all ranks. Frames follow a small camera orbit around the app's
+eye (app.cpp:88): frame k's eye moves along a 0.5-unit circle, so no two frames of a run trace
+the same rays. Frames are rendered F per launch (atr_render_start_cameras: one grid, one camera
+per frame) on S streams; each rank traces its shard tiles into a packed buffer (framebuffer and
+the reference's per-pixel ray_casts); for N > 1 the packed buffers are gathered to rank 0 over
+RCCL (torch.distributed "nccl") and scattered into the frame there, and rank 0 sums
+total_ray_casts (renderer.cpp:465-468). The scene (OBJ load, octree build, upload) and the shard
+plan are prepared before timing; inputs are resident in HBM when the timed region starts.
 
-Extra JSON fields: roofline (render kernel: algorithmic bytes per launch / average launch time
-from HIP events on the launch stream, against 8 TB/s; traffic = HBM bytes per launch from a
-rocprofv3 --pmc child run, FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes),
-cpu_baseline (the C oracle, i.e. the reference algorithm restated, on the host cores of the
-same box, reference tile scheduler).
+value = traced rays of all ranks in the K timed frames (counted by the kernels: every
+get_intersection_data-equivalent call) / max-over-ranks wall time. The K frames are split into
+launches of as equal size as possible (at most F each), so the pipeline's fill and drain are
+the same share of the run whatever K is.
+
+--gpus N > 1 without WORLD_SIZE in the environment: this process starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child before touching
+the GPU and exits with its code. --selftest: no GPU; a synthetic fill (pixel index) stands in
+for the render kernel so the launch, shard plan, gather and frame assembly run on CPU (gloo).
+ATR_DIST_BACKEND=gloo rehearses N ranks on one GPU (host-staged gather).
+
+Extra JSON fields: single_frame (one frame per launch, app camera: kernel time from HIP events
+on the launch stream and its Mrays/s), roofline (that kernel: algorithmic bytes per launch /
+its average duration, against 8 TB/s; traffic = HBM bytes per launch from rocprofv3 --pmc
+FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes of a child run), cpu_baseline
+(the C oracle, i.e. the reference algorithm restated, on the host's cores and on one thread),
+prep (OBJ load, host and device octree build, upload; untimed for Mrays/s).
 """
 import argparse
 import csv
 import glob
 import json
+import math
 import os
 import re
+import socket
 import subprocess
 import sys
 import time
@@ -30,10 +44,14 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-
+METRIC = "Mrays/sec on Dragon.obj 1920x1080 @ 1/2/4/8 GPU; % HBM roofline"
 SEED = 0x853C49E6748FEA9B
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# config -> (asset, W, H, spp, bounces, use_tree)  (BASELINE.json configs, SURVEY.md 8)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+APP_EYE = (0.1, 2.0, 0.0)        # app.cpp:88
+APP_FACING = (-0.1, -0.5, -1.0)
+ORBIT_RADIUS = 0.5
+ORBIT_PERIOD = 256
+# config -> (asset, W, H, spp, bounces, use_tree)  (BASELINE.json configs, SURVEY.md 8(d))
 CONFIGS = {
     "c1": ("Cube", 256, 256, 1, 1, True),
     "c2": ("Monkey", 1280, 720, 1, 1, False),
@@ -42,17 +60,23 @@ CONFIGS = {
     "c5": ("Dragon", 3840, 2160, 256, 5, True),
 }
 GOLDEN_COUNTERS = {"c3": "dragon_1920x1080_tree", "c2": "monkey_1280x720_bf", "c1": "cube_256_tree"}
+MATERIALS = [((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)]  # app.cpp:91-105
+
+
+def orbit_eye(k):
+    a = 2.0 * math.pi * (k % ORBIT_PERIOD) / ORBIT_PERIOD
+    return (APP_EYE[0] + ORBIT_RADIUS * math.sin(a), APP_EYE[1], APP_EYE[2] + ORBIT_RADIUS * (1.0 - math.cos(a)))
 
 
 def algorithmic_bytes_per_ray(ctr):
     """B = 24 (ray) + 12 (hit out) + 28 N_box + 40 N_tri + 8 N_leaf per ray,
-    N_* = the reference's own per-ray work on this input (golden counters, tools/make_goldens.py)."""
+    N_* = the reference's own per-ray work on this input."""
     n = ctr["n_rays"]
     return (36.0 + 28.0 * ctr["n_box"] / n + 40.0 * ctr["n_tri"] / n + 8.0 * ctr["n_leaf"] / n)
 
 
 def cluster_bytes_per_ray(ctr):
-    """The clustered kernel's own algorithmic bytes per ray, in its own data layout (DESIGN.md
+    """The clustered kernels' own algorithmic bytes per ray, in their own data layout (DESIGN.md
     §6): ray in + hit out (36); one 48-B inner-node record per visit, shared by the 8 child boxes
     it tests (6 per box test, re-walks included); 8 per leaf range; 32 per cluster record; the
     screen's 6 (three f16) per screened primitive; a, ab, ac (36) per full triangle test. N_*
@@ -62,10 +86,22 @@ def cluster_bytes_per_ray(ctr):
             + 6.0 * ctr["screened"] / n + 36.0 * ctr["n_tri"] / n)
 
 
-def pmc_traffic(args, kernel_name="render_kernel"):
-    """HBM bytes per render launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a
-    short child run of this benchmark. FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950
-    reports half the bytes of wide reads); both counters are in KB."""
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota if any."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(p))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def pmc_traffic(args, kernel_name):
+    """HBM bytes per one-frame render launch from two rocprofv3 --pmc passes (FETCH_SIZE,
+    WRITE_SIZE) of a short child run of this benchmark. FETCH_SIZE is doubled (MI355X_MICROARCH.md,
+    HBM: gfx950 reports half the bytes of wide reads); both counters are in KB."""
     exe = "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
         return None, "rocprofv3 missing"
@@ -75,11 +111,11 @@ def pmc_traffic(args, kernel_name="render_kernel"):
         os.makedirs(d, exist_ok=True)
         cmd = [exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-               "--frames-per-launch", "1", "--streams", "1",
-               "--config", args.config, "--variant", args.variant, "--no-cpu-baseline", "--no-pmc"]
+               "--frames-per-launch", "1", "--streams", "1", "--config", args.config, "--variant", args.variant,
+               "--no-cpu-baseline", "--no-pmc", "--no-prep"]
         env = dict(os.environ)
-        env.pop("RANK", None)
-        env.pop("WORLD_SIZE", None)
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            env.pop(k, None)
         try:
             subprocess.run(cmd, check=True, timeout=300, env=env, stdout=subprocess.DEVNULL,
                            stderr=subprocess.DEVNULL)
@@ -90,8 +126,8 @@ def pmc_traffic(args, kernel_name="render_kernel"):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
-                    # one-frame launches of the product kernel (not the instrumented COUNT build)
-                    if kernel_name in name and not re.search(r"render_kernel<\d+, true", name) \
+                    # product launches only (not the instrumented COUNT build: <.., true, ..>)
+                    if kernel_name in name and not re.search(kernel_name + r"<(\d+, )?true", name) \
                             and row.get("Counter_Name") == ctr:
                         vals.append(float(row["Counter_Value"]))
         if not vals:
@@ -101,22 +137,69 @@ def pmc_traffic(args, kernel_name="render_kernel"):
 
 
 def cpu_baseline(asset, W, H, spp, bounces, use_tree, seconds):
-    """The reference algorithm (C oracle restatement) on this host: reference tile scheduler
-    (renderer.cpp:403-455) on `threads` pthreads, whole frames until `seconds` elapse."""
+    """The reference algorithm (C oracle restatement) on this host, render time only: (a) on the
+    host's CPU share with the reference tile scheduler (renderer.cpp:403-455) over whole frames
+    when one frame fits the budget, else a strided row sample claimed row by row; (b) on one
+    thread, a strided row sample. Traced rays count every get_intersection_data call (the
+    threaded whole-frame run traces the reference's 1-px tile overlaps twice, as its threads do);
+    ray_casts is the reference's non-sky count (renderer.cpp:260)."""
     from atray_amd.assets import CENTERS, asset_path
     from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
     s = O.Scene(asset_path(asset), center=CENTERS[asset], use_tree=use_tree)
     cam = O.Camera(W, H, spp=spp, bounces=bounces)
-    frames, secs = 0, 0.0
-    while secs < seconds or frames == 0:
-        dt, _, _, _ = s.render_threaded(cam, SEED, threads)
-        secs += dt
-        frames += 1
-    rays = frames * W * H * spp  # traced primary rays; 1 ray per pixel-sample at bounce_limit 1
-    return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} full {asset} {W}x{H} frames spp={spp} bounces={bounces}, "
-                      f"reference tile scheduler ({W // threads}px tiles), {secs:.1f}s of render time"}
+    share = cpu_share()
+
+    def rows_sample(threads, budget):
+        # passes over rows r0, r0 + step, ... (2 x threads rows spread over the frame), r0 = 0, 1,
+        # ... until the budget is spent: every row at most once
+        step = max(1, H // max(4, 2 * threads))
+        secs = traced = casts = done = 0
+        while (secs < budget or done == 0) and done < step:
+            dt, tr, ca = s.render_rows_threaded(cam, SEED, threads, done, step, (H - 1 - done) // step + 1)
+            secs, traced, casts, done = secs + dt, traced + tr, casts + ca, done + 1
+        return secs, traced, casts, f"rows r + {step} k for r < {done}, rows claimed by {threads} threads"
+
+    def frames(threads, budget):
+        secs = traced = casts = nf = 0
+        while secs < budget or nf == 0:
+            dt, _, tot, tr = s.render_threaded(cam, SEED, threads)
+            secs, traced, casts, nf = secs + dt, traced + tr, casts + tot, nf + 1
+        return secs, traced, casts, f"{nf} whole frames, reference tile scheduler ({W // threads}px tiles)"
+
+    rows = []
+    for threads, budget in ((share, 0.6 * seconds), (1, 0.4 * seconds)):
+        per_frame_est = W * H * spp * (1.3 if bounces > 1 else 1.0) / (1.0e6 * threads)  # ~1 Mray/s/thread
+        fn = frames if per_frame_est < budget / 2 else rows_sample
+        secs, traced, casts, how = fn(threads, budget)
+        rows.append({"value": traced / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+                     "sample": f"{asset} {W}x{H} spp={spp} bounces={bounces}: {how}, {traced} traced rays, "
+                               f"{secs:.1f}s of render time", "ray_casts": casts,
+                     "ray_casts_per_s": casts / secs})
+    out = dict(rows[0])
+    out["nproc"] = os.cpu_count()
+    out["cpu_share"] = share
+    out["single_thread"] = rows[1]
+    return out
+
+
+def spawn_ranks(n):
+    """--gpus n without a launcher: run this script under torch.distributed.run as a child (no
+    GPU call in this process), return its exit code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def launch_sizes(k, f):
+    """k frames in launches of at most f, sizes as equal as possible."""
+    if k <= 0:
+        return []
+    n = (k + f - 1) // f
+    return [k // n + (1 if i < k % n else 0) for i in range(n)]
 
 
 def main():
@@ -127,28 +210,111 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps"])
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="launches in flight (one HIP stream each)")
+    ap.add_argument("--no-prep", action="store_true", help="skip the device octree build timing")
+    ap.add_argument("--no-orbit", action="store_true", help="every frame from the app camera")
+    ap.add_argument("--streams", type=int, default=2, help="launches in flight (one HIP stream each)")
     ap.add_argument("--frames-per-launch", type=int, default=8,
-                    help="frames rendered by one launch (atr_render_start_frames); 1 = one frame per launch")
+                    help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
                     help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
     ap.add_argument("--check", action="store_true",
-                    help="rank 0: compare the assembled frame with a one-launch full-frame render")
-    ap.add_argument("--hw-queues", type=int, default=0,
-                    help="GPU_MAX_HW_QUEUES floor for this process (0 = leave the environment alone)")
+                    help="rank 0: compare every assembled frame with a one-launch full-frame render")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU only: synthetic fill instead of the render kernel (launch/plan/gather test)")
     args = ap.parse_args()
-    # Frames in flight run on separate HIP streams; HIP maps a process's streams onto
-    # GPU_MAX_HW_QUEUES hardware queues (default 4, shared with RCCL's streams), and streams on
-    # one queue serialize. Read at HIP initialization, so set before torch loads.
-    if args.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < args.hw_queues:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
+    args.frames_per_launch = max(1, min(16, args.frames_per_launch))
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.selftest:
+        return selftest(args)
+    return run(args)
+
+
+def frame_assembly(plan, F, world):
+    """Destination of every slot of the gathered buffer [world][2][F][maxn] (framebuffer frames,
+    then ray_casts frames) in a buffer holding F frame images and F ray_casts images, each W*H + 1
+    long (the extra element takes the plan's padding slots)."""
+    import numpy as np
+    from atray_amd import shard as S
+    npx = plan.width * plan.height + 1
+    one = S.assembly_index(plan).reshape(world, 1, 1, plan.max_size)
+    part = np.arange(2, dtype=np.int64).reshape(1, 2, 1, 1) * (F * npx)
+    frame = np.arange(F, dtype=np.int64).reshape(1, 1, F, 1) * npx
+    return np.ascontiguousarray(one + part + frame).ravel()
+
+
+def selftest(args):
+    """Launch + shard plan + gather + assembly on CPU (gloo) with a synthetic fill: rank r writes
+    pixel index + 7 f into its packed framebuffer slots of frame f and (pixel % 5) into ray_casts.
+    Rank 0 checks every assembled frame and the total_ray_casts sum."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from atray_amd import shard as S
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    asset, W, H = CONFIGS[args.config][:3]
+    W, H = min(W, 480), min(H, 272)  # keep the CPU run small
+    side = min(args.side, 32)
+    n = len(S.E.shard_grid(W, H, side))
+    costs = (np.arange(n) * 7919) % 97 + 1  # deterministic stand-in for the calibration render
+    plan = S.ShardPlan.balanced(costs, W, H, world, side, args.rank0_extra) if args.plan == "cost" \
+        else S.ShardPlan(W, H, world, side)
+    F = args.frames_per_launch
+    pix = plan.pixel_map(rank)
+    maxn = plan.max_size
+    dst = torch.from_numpy(frame_assembly(plan, F, world))
+    mism, casts_ok, frames = 0, True, 0
+    t0 = time.perf_counter()
+    for j, nf in enumerate(launch_sizes(args.steps, F)):
+        buf = torch.zeros(2 * F * maxn, dtype=torch.int64)
+        for f in range(nf):
+            k = j * F + f
+            buf[f * maxn:f * maxn + len(pix)] = torch.from_numpy(pix + 7 * k)
+            buf[(F + f) * maxn:(F + f) * maxn + len(pix)] = torch.from_numpy(pix % 5)
+        big = torch.zeros(world * 2 * F * maxn, dtype=torch.int64)
+        if world > 1:
+            dist.gather(buf, list(big.chunk(world)) if rank == 0 else None, dst=0)
+        else:
+            big.copy_(buf)
+        if rank == 0:
+            npx = W * H + 1
+            img = torch.zeros(2 * F * npx, dtype=torch.int64)
+            img.index_copy_(0, dst, big)
+            want = np.arange(W * H, dtype=np.int64)
+            for f in range(nf):
+                k = j * F + f
+                got = img[f * npx:f * npx + W * H].numpy()
+                mism += int((got != want + 7 * k).sum())
+                casts = img[(F + f) * npx:(F + f) * npx + W * H].numpy()
+                casts_ok &= int(casts.sum()) == int((want % 5).sum())
+                frames += 1
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 4),
+                          "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+                          "data": "selftest: synthetic fill, no GPU", "selftest": True,
+                          "config": {"workload": f"{args.config} plan/gather selftest {W}x{H}",
+                                     "parallelism": f"tiles{world}", "shard_pixels": [int(x) for x in plan.sizes]},
+                          "frames_checked": frames, "check_mismatched_pixels": mism,
+                          "total_ray_casts_ok": bool(casts_ok)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run(args):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -175,62 +341,81 @@ def main():
                "tile": E.ATR_KERNEL_TILE, "tile8": E.ATR_KERNEL_TILE8,
                "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
                "ps": E.ATR_KERNEL_PERSIST}[args.variant]
-    mesh = E.Mesh.load_obj(asset_path(asset))
+    # ---- scene prep (untimed for Mrays/s; reported under "prep")
+    prep = {}
+    path = asset_path(asset)
+    t = time.perf_counter()
+    mesh = E.Mesh.load_obj(path)  # load_model_data, parallel chunks (OBJ_loader.cpp:298-340)
+    prep["obj_load_ms"] = round((time.perf_counter() - t) * 1e3, 2)
     box = mesh.translate_to(mesh.aabb(), CENTERS[asset])
-    tree = E.Octree.build(mesh, 300) if use_tree else None
+    tree = None
+    if use_tree:
+        t = time.perf_counter()
+        tree = E.Octree.build(mesh, 300)
+        prep["octree_host_ms"] = round((time.perf_counter() - t) * 1e3, 2)
     eng = E.Engine(local % ndev)
-    eng.upload([((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)],
-               [(mesh, tree, box, 1)])
-    cam = E.camera(W, H, spp, bounces)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    if use_tree and not args.no_prep and rank == 0:
+        tm = {}
+        E.Octree.build_device(mesh, 300, local % ndev, timings=tm)  # f3: same tree on the GPU
+        prep["octree_device_ms"] = round(tm["wall_ms"], 2)
+        prep["octree_device_kernel_ms"] = round(tm["device_ms"], 3)
+    t = time.perf_counter()
+    eng.upload(MATERIALS, [(mesh, tree, box, 1)])
+    torch.cuda.synchronize()
+    prep["upload_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+    prep["scene_device_bytes"] = eng.scene_info()["device_bytes"]
+    app_cam = E.camera(W, H, spp, bounces)
+    n_orbit = 1 if args.no_orbit else ORBIT_PERIOD
+    cams = [app_cam if args.no_orbit else E.camera(W, H, spp, bounces, eye=orbit_eye(k), facing=APP_FACING)
+            for k in range(n_orbit)]
 
-    # shard plan (scene prep, untimed): one calibration render measures every grid tile's cost
-    # on rank 0, broadcast so all ranks derive the same longest-first deal
+    # ---- shard plan (untimed): one calibration render measures every grid tile's cost on rank 0,
+    # broadcast so all ranks derive the same longest-first deal
     if world > 1 and args.plan == "cost":
-        costs = S.tile_costs(eng, cam, W, H, args.side, SEED) if rank == 0 else np.zeros(
+        costs = S.tile_costs(eng, app_cam, W, H, args.side, SEED) if rank == 0 else np.zeros(
             len(E.shard_grid(W, H, args.side)), np.int64)
         costs = S.shared_costs(costs, rank, dist, dev if backend == "nccl" else "cpu")
         plan = S.ShardPlan.balanced(costs, W, H, world, args.side, args.rank0_extra)
     else:
         plan = S.ShardPlan(W, H, world, args.side)
     sizes, maxn = plan.sizes, plan.max_size
-    tiles = E.tiles_array(plan.tiles[rank])
-    # Frames in flight: launch j renders frames jF .. jF+F-1 (F = --frames-per-launch, one grid:
-    # a frame's slow cells overlap the other frames') on stream j % S (S = --streams, output
-    # buffers per stream); for N > 1 the launch's F packed frames are gathered to rank 0 in ONE
-    # gather on that stream and assembled there with ONE index_copy_ while later launches run.
-    S_, F_ = max(1, args.streams), max(1, args.frames_per_launch)
-    # frame slots on streams of their own (not the null stream, which HIP orders against the
-    # process's blocking streams)
+    tiles = E.tiles_array(plan.tiles[rank]) if world > 1 else E.tiles_array([[0, 0, W - 1, H - 1]])
+    S_, F_ = max(1, args.streams), args.frames_per_launch
     streams = [torch.cuda.Stream(dev) for _ in range(S_)]
     npf = W * H if world == 1 else maxn  # output elements per frame (stride between frames)
-    outbuf = [torch.zeros(F_ * npf, dtype=torch.int32, device=dev) for _ in range(S_)]
+    # per stream slot: [F framebuffers][F ray_casts] (u32 each) and a traced-ray accumulator
+    outbuf = [torch.zeros(2 * F_ * npf, dtype=torch.int32, device=dev) for _ in range(S_)]
+    traced = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
     on_host = world > 1 and backend != "nccl"
     images = None
-    if world == 1:
-        images = [outbuf[q][f * npf:(f + 1) * npf] for q in range(S_) for f in range(F_)]
-    elif rank == 0:
-        # per stream slot: every rank's F packed frames [world x F x maxn]; one index_copy_ through
-        # the plan's assembly index (padding -> a trash pixel past each frame) writes F images
-        big = [torch.zeros(world * F_ * maxn, dtype=torch.int32, device="cpu" if on_host else dev)
+    if world > 1 and rank == 0:
+        big = [torch.zeros(world * 2 * F_ * maxn, dtype=torch.int32, device="cpu" if on_host else dev)
                for _ in range(S_)]
-        gather = [[b_[r * F_ * maxn:(r + 1) * F_ * maxn] for r in range(world)] for b_ in big]
-        one = S.assembly_index(plan).reshape(world, 1, maxn)
-        dst_all = one + (np.arange(F_, dtype=np.int64) * (W * H + 1)).reshape(1, F_, 1)
-        dst_idx = torch.from_numpy(np.ascontiguousarray(dst_all).ravel()).to(dev)
-        images_ext = [torch.zeros(F_ * (W * H + 1), dtype=torch.int32, device=dev) for _ in range(S_)]
-        images = [im[f * (W * H + 1):f * (W * H + 1) + W * H] for im in images_ext for f in range(F_)]
-        staging = torch.zeros(world * F_ * maxn, dtype=torch.int32, device=dev) if on_host else None
-    traced = torch.zeros(1, dtype=torch.int64, device=dev)
+        gather = [list(b_.chunk(world)) for b_ in big]
+        dst_idx = torch.from_numpy(frame_assembly(plan, F_, world)).to(dev)
+        images = [torch.zeros(2 * F_ * (W * H + 1), dtype=torch.int32, device=dev) for _ in range(S_)]
+        staging = torch.zeros(world * 2 * F_ * maxn, dtype=torch.int32, device=dev) if on_host else None
     layout = E.ATR_LAYOUT_IMAGE if world == 1 else E.ATR_LAYOUT_PACKED
-    frames = [E.atr_frame(layout, outbuf[q].data_ptr(), None, None, None, None, None) for q in range(S_)]
+
+    def frame_of(q, nf_cap=F_):
+        base = outbuf[q].data_ptr()
+        return E.atr_frame(layout, base, None, None, None, base + 4 * nf_cap * npf, traced[q].data_ptr())
+
     pending = {}
+
+    def image_views(q, f):
+        """(framebuffer, ray_casts) of frame f of stream slot q as (H*W,) views."""
+        if world == 1:
+            b = outbuf[q]
+            return b[f * npf:(f + 1) * npf], b[(F_ + f) * npf:(F_ + f + 1) * npf]
+        npx = W * H + 1
+        im = images[q]
+        return im[f * npx:f * npx + W * H], im[(F_ + f) * npx:(F_ + f) * npx + W * H]
 
     def assemble(j):
         """Launch j's gather done (its stream waits on it); rank 0 scatters every rank's packed
         frames into that slot's images, on the launch's stream."""
-        q = j % S_
-        work = pending.pop(j)
+        q, work = pending.pop(j)
         with torch.cuda.stream(streams[q]):
             if work is not None:
                 work.wait()
@@ -239,106 +424,128 @@ def main():
                 if on_host:
                     staging.copy_(src, non_blocking=False)
                     src = staging
-                images_ext[q].index_copy_(0, dst_idx, src)
+                images[q].index_copy_(0, dst_idx, src)
 
-    def launch(j, nf, fr=None):
-        q = j % S_
+    def launch(j, k0, nf, q):
         if j - S_ in pending:
             assemble(j - S_)  # before this slot's buffers are reused
-        eng.render_start_frames(cam, tiles, fr or frames[q], nf, npf, SEED, stream=streams[q].cuda_stream,
-                                variant=variant)
-        if world == 1:
-            return
-        with torch.cuda.stream(streams[q]):
-            buf = outbuf[q]
-            if on_host:
-                torch.cuda.synchronize()
-                buf = buf.cpu()
-            pending[j] = dist.gather(buf, gather[q] if rank == 0 else None, dst=0, async_op=True)
+        fr = [cams[(k0 + f) % n_orbit] for f in range(nf)]
+        eng.render_start_cameras(fr, tiles, frame_of(q), npf, SEED, stream=streams[q].cuda_stream, variant=variant)
+        if world > 1:
+            with torch.cuda.stream(streams[q]):
+                buf = outbuf[q]
+                if on_host:
+                    torch.cuda.synchronize()
+                    buf = buf.cpu()
+                pending[j] = (q, dist.gather(buf, gather[q] if rank == 0 else None, dst=0, async_op=True))
+        else:
+            pending[j] = (q, None)
 
-    def run_steps(n):
-        for j in range((n + F_ - 1) // F_):
-            launch(j, min(F_, n - j * F_))
+    def run_frames(k0, k, on_launch=None):
+        j0 = 0
+        for nf in launch_sizes(k, F_):
+            q = j0 % S_
+            launch(j0, k0, nf, q)
+            if on_launch:
+                on_launch(j0, k0, nf, q)
+            k0 += nf
+            j0 += 1
         for j in sorted(pending):
             assemble(j)
 
-    torch.cuda.synchronize()  # buffers were zero-filled on the current stream
-    # rays per frame (all ranks): counted by the kernel (every get_intersection_data call)
-    launch(0, 1, E.atr_frame(layout, outbuf[0].data_ptr(), None, None, None, None, traced.data_ptr()))
-    for j in sorted(pending):
-        assemble(j)
     torch.cuda.synchronize()
-    rays_t = traced.clone() if backend == "nccl" or world == 1 else traced.cpu()
-    if world > 1:
-        dist.all_reduce(rays_t)
-    rays_per_step = int(rays_t.item())
-
-    run_steps(args.warmup)
+    run_frames(0, args.warmup)
+    torch.cuda.synchronize()
+    for t_ in traced:
+        t_.zero_()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(args.steps)
+    run_frames(args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rays = torch.stack(traced).sum().reshape(1)
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    # roofline: the render kernel's own average duration, launches serialized on one stream
-    # (HIP events on that stream; rocprofv3 of `bench.py --streams 1` reports the same kernel)
+        rays = rays if backend == "nccl" else rays.cpu()
+        dist.all_reduce(rays)
+    rays_total = int(rays.item())
+
+    # ---- check (rank 0): the last S x F frames in the slots against one-launch full-frame renders
+    check = None
+    casts_total = None
+    if rank == 0:
+        ref = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        refc = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        sizes_l = launch_sizes(args.steps, F_)
+        k0 = args.warmup
+        last = {}
+        for j, nf in enumerate(sizes_l):
+            last[j % S_] = (k0, nf)
+            k0 += nf
+        casts_total = 0
+        mism = 0
+        for q, (kk, nf) in sorted(last.items()):
+            for f in range(nf):
+                fb, cs = image_views(q, f)
+                casts_total += int(cs.to(torch.int64).sum().item())
+                if args.check:
+                    fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, ref.data_ptr(), None, None, None, refc.data_ptr(), None)
+                    eng.render_start(cams[(kk + f) % n_orbit], [[0, 0, W - 1, H - 1]], fr, SEED,
+                                     stream=torch.cuda.current_stream(dev).cuda_stream)
+                    torch.cuda.synchronize()
+                    mism += int((ref != fb).sum().item()) + int((refc != cs).sum().item())
+        check = mism if args.check else None
+        casts_frames = sum(nf for _, nf in last.values())
+
+    # ---- single frame (app camera, one frame per launch): the roofline kernel
+    s0 = streams[0]
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
     for a, b in evs:
-        a.record(streams[0])
-        eng.render_start(cam, tiles, frames[0], SEED, stream=streams[0].cuda_stream, variant=variant)
-        b.record(streams[0])
+        a.record(s0)
+        eng.render_start(app_cam, tiles, frame_of(0), SEED, stream=s0.cuda_stream, variant=variant)
+        b.record(s0)
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     rc, _ = eng.wait()
     assert rc == 0
-    # the dominant kernel's work on this rank's tiles, counted by the instrumented build of the
-    # same variant (untimed; deterministic)
-    live_ctr = eng.counters(cam, tiles, SEED, variant) if rank == 0 else None
-    check = None
-    if args.check and rank == 0:
-        ref = torch.zeros(W * H, dtype=torch.int32, device=dev)
-        fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, ref.data_ptr(), None, None, None, None, None)
-        eng.render_start(cam, [[0, 0, W - 1, H - 1]], fr, SEED, stream=stream)
-        torch.cuda.synchronize()
-        # images holding a frame: stream slot j % S, position f of launch j
-        used = sorted({((k // F_) % S_) * F_ + k % F_ for k in range(max(args.steps, args.warmup))})
-        check = sum(int((ref != images[q]).sum().item()) for q in used)
+    live_ctr = eng.counters(app_cam, tiles, SEED, variant) if rank == 0 else None
 
     if rank == 0:
-        value = rays_per_step * args.steps / elapsed / 1e6
-        out = {"metric": "Mrays/sec on Dragon.obj 1920x1080 @ 1/2/4/8 GPU; % HBM roofline",
-               "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+        value = rays_total / elapsed / 1e6
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-               "data": "synthetic: the survey's Dragon surrogate (Dragon.obj absent), app camera/materials",
+               "data": "synthetic: the survey's Dragon surrogate (Dragon.obj absent), app materials, "
+                       + ("app camera every frame" if args.no_orbit else
+                          f"camera orbit r={ORBIT_RADIUS} around the app eye, {ORBIT_PERIOD} distinct frames"),
                "config": {"workload": f"{args.config}: {asset} {W}x{H} spp={spp} bounces={bounces} "
                                       f"{'octree' if use_tree else 'brute-force'}",
-                          "rays_per_step": rays_per_step, "shard_tile": args.side,
+                          "rays_per_step": round(rays_total / args.steps), "shard_tile": args.side,
                           "parallelism": f"tiles{world}", "kernel": args.variant,
                           "plan": args.plan if world > 1 else "single",
-                          "frames_in_flight": args.streams * args.frames_per_launch,
-                          "streams": args.streams, "frames_per_launch": args.frames_per_launch,
-                          "shard_pixels": [int(x) for x in sizes]}}
+                          "streams": args.streams, "frames_per_launch": F_,
+                          "launches": launch_sizes(args.steps, F_),
+                          "shard_pixels": [int(x) for x in sizes]},
+               "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
         if check is not None:
             out["check_mismatched_pixels"] = check
+        n1 = live_ctr["n_rays"]
+        out["single_frame"] = {"kernel_ms": round(kern_ms, 4), "mrays_s": round(n1 / kern_ms / 1e3, 1),
+                               "camera": "app", "rays": n1}
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
         clustered = args.variant in ("auto", "cl", "ps")
-        if clustered:
-            bpr = cluster_bytes_per_ray(live_ctr)
-        else:
-            bpr = algorithmic_bytes_per_ray(live_ctr)
-        achieved = bpr * live_ctr["n_rays"] / (kern_ms * 1e-3) / 1e9
+        bpr = cluster_bytes_per_ray(live_ctr) if clustered else algorithmic_bytes_per_ray(live_ctr)
+        achieved = bpr * n1 / (kern_ms * 1e-3) / 1e9
         roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "bytes_per_ray": round(bpr, 1), "rays_per_launch": live_ctr["n_rays"],
+                     "bytes_per_ray": round(bpr, 1), "rays_per_launch": n1,
                      "model": "clustered scan, own work (DESIGN.md 6)" if clustered
                      else "reference work (SURVEY.md 8(d))"})
         gname = GOLDEN_COUNTERS.get(args.config)
@@ -347,12 +554,16 @@ def main():
                 ctr = json.load(f)["hits"][gname]["counters"]
             rbpr = algorithmic_bytes_per_ray(ctr)
             roof["ref_bytes_per_ray"] = round(rbpr, 1)
-            roof["ref_equivalent_GBs"] = round(rbpr * live_ctr["n_rays"] / (kern_ms * 1e-3) / 1e9, 1)
+            roof["ref_equivalent_GBs"] = round(rbpr * n1 / (kern_ms * 1e-3) / 1e9, 1)
+        prim = bounces == 1  # AUTO: CLUSTER cells for primary-only renders, PERSIST otherwise
+        kname = "persist_kernel" if args.variant == "ps" or (args.variant == "auto" and not prim) else "render_kernel"
+        roof["kernel"] = kname
         if world == 1 and not args.no_pmc:
-            traffic, why = pmc_traffic(args)
+            traffic, why = pmc_traffic(args, kname)
             roof["traffic"] = traffic
             roof["traffic_note"] = why
         out["roofline"] = roof
+        out["prep"] = prep
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(asset, W, H, spp, bounces, use_tree, args.cpu_seconds)
             out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)

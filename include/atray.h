@@ -48,15 +48,28 @@ typedef struct atr_mesh atr_mesh;
 typedef struct atr_octree atr_octree;
 
 /* load_model_data (OBJ_loader.h:6): custom parse_f64 (parser.h:113-191), faces keep the first
-   triangle of each polygon, negative indices relative to the end. */
+   triangle of each polygon, negative indices relative to the end. atr_mesh_load_obj parses on
+   the host's threads (threads = min(hardware threads, 16), ATR_PARSE_THREADS overrides);
+   atr_mesh_parse_obj on one. */
 int atr_mesh_load_obj(const char* path, atr_mesh** out);
 int atr_mesh_parse_obj(const char* text, size_t len, atr_mesh** out);
+/* The reference's parallel load (OBJ_loader.cpp:298-340): the text split into `threads`
+   newline-aligned chunks parsed concurrently and joined in order (join_chunks, :190-227), then
+   the relative indices resolved (prep_model_data, :229-267). threads = 0 picks the default.
+   The mesh is bit-identical for every thread count. */
+int atr_mesh_load_obj_threaded(const char* path, int32_t threads, atr_mesh** out);
+int atr_mesh_parse_obj_threaded(const char* text, size_t len, int32_t threads, atr_mesh** out);
 /* ModelData from caller arrays (copied). normals may be NULL (flat shading). */
 int atr_mesh_from_arrays(const float* vertices, uint32_t nvertices, const int32_t* face_vertices,
                          uint32_t nfaces, const float* normals, uint32_t nnormals,
                          const int32_t* face_normals, atr_mesh** out);
 void atr_mesh_free(atr_mesh* m);
 int atr_mesh_info(const atr_mesh* m, uint32_t* nvertices, uint32_t* nnormals, uint32_t* nfaces);
+/* Copy ModelData out (any pointer may be NULL): 3 floats per vertex / normal / texcoord, 3 ints
+   per face for each index array (0-based, -1 = absent). ntexcoords (may be NULL) receives the
+   texcoord count. */
+int atr_mesh_export(const atr_mesh* m, float* vertices, float* normals, float* texcoords, uint32_t* ntexcoords,
+                    int32_t* face_v, int32_t* face_t, int32_t* face_n);
 /* get_AABB (model.h:41-61): min xyz, max xyz padded by 1e-4. */
 int atr_mesh_aabb(const atr_mesh* m, float aabb_out[6]);
 /* translate_to (model.h:136-152): moves the vertices and the caller's AABB (in/out). */
@@ -196,6 +209,13 @@ int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
 int atr_render_start_frames(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                             const atr_frame* frame, int32_t nframes, int64_t frame_stride, uint64_t seed,
                             void* stream, int32_t variant);
+/* The same with one camera per frame (an animation, a camera path): frame f renders cams[f]
+   (1 <= nframes <= 16). All cameras must share width, height, samples_per_pixel, bounce_limit
+   and anti_aliasing (ATR_E_INVALID otherwise); eye, facing and field of view may differ. Every
+   frame equals atr_render_start_ex's output for its camera. */
+int atr_render_start_cameras(atr_ctx* ctx, const atr_camera* cams, int32_t nframes, const atr_tile* tiles,
+                             int32_t ntiles, const atr_frame* frame, int64_t frame_stride, uint64_t seed,
+                             void* stream, int32_t variant);
 /* Diagnostic, synchronous: an instrumented render of the same work that returns
    [0] traced rays, [1] box tests, [2] triangle tests, [3] leaves scanned -- the reference's own
    per-ray work on this input (kd_tree.cpp:337-465) for every variant but CLUSTER, whose [2]

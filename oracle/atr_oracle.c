@@ -768,11 +768,13 @@ typedef struct {
     const om_scene* s; const om_camera* cm; uint64_t seed;
     const int32_t* tiles; int32_t ntiles; volatile int32_t next;
     uint32_t* fb; int64_t* tile_casts; int32_t maxn;
+    volatile uint64_t traced; /* get_intersection_data calls, summed over the threads */
 } pool_t;
 
 static void* tile_worker(void* arg) { /* start_tile_render_thread (:371-399) */
     pool_t* p = (pool_t*)arg;
     trav_ws w; ws_init(&w, p->maxn);
+    om_counters ctr; memset(&ctr, 0, sizeof(ctr));
     for (;;) {
         int32_t k = __atomic_add_fetch(&p->next, 1, __ATOMIC_SEQ_CST); /* :298-307 */
         if (k > p->ntiles) break;
@@ -781,14 +783,65 @@ static void* tile_worker(void* arg) { /* start_tile_render_thread (:371-399) */
         for (int32_t y = t[1]; y <= t[3]; y++)
             for (int32_t x = t[0]; x <= t[2]; x++) {
                 ov3 rgb; uint32_t px, c;
-                render_pixel(p->s, p->cm, p->seed, x, y, &w, NULL, &rgb, &px, &c);
+                render_pixel(p->s, p->cm, p->seed, x, y, &w, &ctr, &rgb, &px, &c);
                 p->fb[(size_t)y * p->cm->width + x] = px;
                 casts += c;
             }
         p->tile_casts[k - 1] = casts;
     }
+    __atomic_add_fetch(&p->traced, ctr.n_rays, __ATOMIC_SEQ_CST);
     ws_free(&w);
     return NULL;
+}
+
+/* CPU-baseline sample: rows row0, row0 + row_step, ... (nrows of them) of the frame, claimed one
+   row at a time by `threads` workers (the reference's atomic claim, renderer.cpp:298-307, with a
+   row as the unit), full spp / bounces per pixel. Returns seconds; traced rays and the
+   reference's non-sky ray_casts (renderer.cpp:260) of the sample through the pointers. */
+typedef struct {
+    const om_scene* s; const om_camera* cm; uint64_t seed;
+    int32_t row0, row_step, nrows; volatile int32_t next; int32_t maxn;
+    volatile uint64_t traced; volatile int64_t casts;
+} rowpool_t;
+
+static void* row_worker(void* arg) {
+    rowpool_t* p = (rowpool_t*)arg;
+    trav_ws w; ws_init(&w, p->maxn);
+    om_counters ctr; memset(&ctr, 0, sizeof(ctr));
+    int64_t casts = 0;
+    for (;;) {
+        int32_t k = __atomic_fetch_add(&p->next, 1, __ATOMIC_SEQ_CST);
+        if (k >= p->nrows) break;
+        const int32_t y = p->row0 + k * p->row_step;
+        for (int32_t x = 0; x < p->cm->width; x++) {
+            ov3 rgb; uint32_t px, c;
+            render_pixel(p->s, p->cm, p->seed, x, y, &w, &ctr, &rgb, &px, &c);
+            casts += c;
+        }
+    }
+    __atomic_add_fetch(&p->traced, ctr.n_rays, __ATOMIC_SEQ_CST);
+    __atomic_add_fetch(&p->casts, casts, __ATOMIC_SEQ_CST);
+    ws_free(&w);
+    return NULL;
+}
+
+double om_render_rows_threaded(const om_scene* s, const om_camera* cm, uint64_t seed, int32_t threads,
+                               int32_t row0, int32_t row_step, int32_t nrows, uint64_t* traced_rays,
+                               int64_t* ray_casts) {
+    rowpool_t p; memset(&p, 0, sizeof(p));
+    p.s = s; p.cm = cm; p.seed = seed; p.row0 = row0; p.row_step = row_step; p.nrows = nrows;
+    p.maxn = 1;
+    for (int32_t i = 0; i < s->nmodels; i++) if (s->models[i].tree && s->models[i].tree->nnodes > p.maxn) p.maxn = s->models[i].tree->nnodes;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int32_t i = 0; i < threads; i++) pthread_create(&th[i], NULL, row_worker, &p);
+    for (int32_t i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (traced_rays) *traced_rays = p.traced;
+    if (ray_casts) *ray_casts = p.casts;
+    free(th);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
 double om_render_threaded(const om_scene* s, const om_camera* cm, uint64_t seed, int32_t threads,
@@ -808,14 +861,11 @@ double om_render_threaded(const om_scene* s, const om_camera* cm, uint64_t seed,
     for (int32_t i = 0; i < threads; i++) pthread_join(th[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     int64_t tot = 0;
-    uint64_t traced = 0;
     for (int32_t i = 0; i < nt; i++) tot += p.tile_casts[i];
-    for (int32_t i = 0; i < nt; i++) {
-        const int32_t* t = &tiles[4 * i];
-        traced += (uint64_t)(t[2] - t[0] + 1) * (uint64_t)(t[3] - t[1] + 1);
-    }
     if (total_ray_casts) *total_ray_casts = tot;
-    if (traced_rays) *traced_rays = traced; /* pixels traced incl. the 1-px tile overlaps */
+    /* every get_intersection_data call, the 1-px tile overlaps traced twice as the reference's
+       threads do */
+    if (traced_rays) *traced_rays = p.traced;
     free(th); free(p.tile_casts); free(tiles);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

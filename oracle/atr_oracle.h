@@ -121,6 +121,11 @@ void om_render_rows(const om_scene* s, const om_camera* cm, uint64_t seed, int32
    claim; returns wall seconds of the render (load/build excluded). */
 double om_render_threaded(const om_scene* s, const om_camera* cm, uint64_t seed, int32_t threads,
                           uint32_t* fb_out, int64_t* total_ray_casts, uint64_t* traced_rays);
+/* CPU-baseline sample: rows row0 + k * row_step (k < nrows), full spp / bounces, claimed a row at
+   a time by `threads` pthreads; returns wall seconds, traced rays and ray_casts of the sample. */
+double om_render_rows_threaded(const om_scene* s, const om_camera* cm, uint64_t seed, int32_t threads,
+                               int32_t row0, int32_t row_step, int32_t nrows, uint64_t* traced_rays,
+                               int64_t* ray_casts);
 /* Tile grid of renderer.cpp:403-445 (inclusive rects). Returns count; writes 4 ints/tile. */
 int32_t om_make_tiles(int32_t width, int32_t height, int32_t threads, int32_t* tiles_out, int32_t cap);
 

@@ -124,6 +124,9 @@ def lib():
         L.om_render_threaded.argtypes = [P(om_scene), P(om_camera), C.c_uint64, C.c_int32,
                                          C.c_void_p, P(C.c_int64), P(C.c_uint64)]
         L.om_render_threaded.restype = C.c_double
+        L.om_render_rows_threaded.argtypes = [P(om_scene), P(om_camera), C.c_uint64, C.c_int32, C.c_int32,
+                                              C.c_int32, C.c_int32, P(C.c_uint64), P(C.c_int64)]
+        L.om_render_rows_threaded.restype = C.c_double
         L.om_make_tiles.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32]
         L.om_make_tiles.restype = C.c_int32
         L.om_pcg_u32.argtypes = [P(C.c_uint64), C.c_uint64]
@@ -268,6 +271,14 @@ class Scene:
                              _ptr(fb), _ptr(casts), C.byref(ctr))
         shp = (y1 - y0, cam.width)
         return rgb.reshape(shp + (3,)), fb.reshape(shp), casts.reshape(shp), ctr.as_dict()
+
+    def render_rows_threaded(self, cam: Camera, seed: int, threads: int, row0: int, row_step: int, nrows: int):
+        """(seconds, traced rays, ray_casts) of a strided row sample on `threads` threads."""
+        traced = C.c_uint64(0)
+        casts = C.c_int64(0)
+        secs = lib().om_render_rows_threaded(C.byref(self.s), C.byref(cam.c), C.c_uint64(seed), int(threads),
+                                             int(row0), int(row_step), int(nrows), C.byref(traced), C.byref(casts))
+        return secs, int(traced.value), int(casts.value)
 
     def render_threaded(self, cam: Camera, seed: int, threads: int):
         fb = np.zeros(cam.width * cam.height, np.uint32)

@@ -1,0 +1,57 @@
+"""bench.py on CPU: `--gpus N` starts N ranks itself (torch.distributed.run child, gloo here) and
+the shard plan + gather + frame assembly reproduce every frame; the launch split does not depend
+on the step count beyond rounding. The render kernel itself runs only on the GPU box (-m gpu);
+here --selftest puts a synthetic fill (pixel index) in its place."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--selftest",
+                        "--steps", "11", "--warmup", "1", "--frames-per-launch", "4"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == n and d["selftest"] is True
+    assert d["frames_checked"] == 11
+    assert d["check_mismatched_pixels"] == 0 and d["total_ray_casts_ok"] is True
+    assert sum(d["config"]["shard_pixels"]) == 480 * 272
+
+
+def test_bench_rejects_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--selftest"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.parametrize("k,f", [(20, 8), (48, 8), (7, 8), (1, 1), (17, 16), (0, 8)])
+def test_launch_sizes_are_balanced(k, f):
+    s = bench.launch_sizes(k, f)
+    assert sum(s) == k and all(1 <= x <= f for x in s)
+    assert (max(s) - min(s) <= 1) if s else k == 0
+    assert len(s) == (k + f - 1) // f
+
+
+def test_orbit_cameras_are_distinct():
+    eyes = {bench.orbit_eye(k) for k in range(bench.ORBIT_PERIOD)}
+    assert len(eyes) == bench.ORBIT_PERIOD
+    assert bench.orbit_eye(0) == bench.APP_EYE

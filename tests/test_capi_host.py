@@ -90,14 +90,67 @@ def test_octree_from_nodes_roundtrip():
         E.Octree.from_nodes(bounds, nodes["children"], nodes["prim_off"], bad, tri, face)
 
 
+QUIRKY = ("# c\nv 0.1 0.2 0.3\nv 1e1 -2.5E-1 +3\nv 1 1 1\nv 2 2 2\nvt 0.5 0.5\nvn 0 0 1\n"
+          "f 1/1/1 2/1/1 3/1/1 4/1/1\nf -4//1 -3//1 -2//1\nusemtl x\r\nv\t3 4 5\nvn 0 1 0\r\n"
+          "f 1 2 3\nf 5//-1 -2//2 1//1\nf 1/1 2/-1 3/1")
+
+
+def _bits(a):
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+def _mesh_equal(a, b):
+    return all(x.shape == y.shape and np.array_equal(_bits(x), _bits(y)) for x, y in zip(a, b))
+
+
 def test_mesh_parser_matches_oracle_on_quirky_text():
-    txt = ("# c\nv 0.1 0.2 0.3\nv 1e1 -2.5E-1 +3\nv 1 1 1\nv 2 2 2\nvt 0.5 0.5\nvn 0 0 1\n"
-           "f 1/1/1 2/1/1 3/1/1 4/1/1\nf -4//1 -3//1 -2//1\nusemtl x\nf 1 2 3")
-    m = E.Mesh.parse_obj(txt)
-    assert m.info() == (4, 1, 3)
-    s = O.Scene(obj_text=txt, center=None, use_tree=False)
+    m = E.Mesh.parse_obj(QUIRKY)
+    assert m.info() == (4, 2, 5)
+    s = O.Scene(obj_text=QUIRKY, center=None, use_tree=False)
     V, N, FV, FN = s.mesh_arrays()
+    ev, en, _, efv, _, efn = m.arrays()
+    assert np.array_equal(ev.view(np.uint32), V.view(np.uint32)) and np.array_equal(en.view(np.uint32), N.view(np.uint32))
+    assert np.array_equal(efv, FV) and np.array_equal(efn, FN)
     assert np.array_equal(m.aabb().view(np.uint32), s.surrounding_aabb.view(np.uint32))
+
+
+@pytest.mark.parametrize("asset", ["Cube", "Monkey", "Deer", "Dragon"])
+def test_parallel_obj_load_bit_identical(asset):
+    """f3: load_model_data's chunked parallel parse (OBJ_loader.cpp:298-340) gives the
+    single-threaded mesh for every chunk count, and both equal the oracle's parse."""
+    one = E.Mesh.load_obj(asset_path(asset), threads=1).arrays()
+    for th in (2, 3, 7, 16, 0):
+        assert _mesh_equal(E.Mesh.load_obj(asset_path(asset), threads=th).arrays(), one), th
+    if asset != "Dragon":  # the Dragon surrogate is checked through the octree test above
+        s = O.Scene(asset_path(asset), center=None, use_tree=False)
+        V, N, FV, FN = s.mesh_arrays()
+        assert np.array_equal(one[0].view(np.uint32), V.view(np.uint32)) and np.array_equal(one[3], FV)
+        assert np.array_equal(one[1].view(np.uint32), N.view(np.uint32)) and np.array_equal(one[5], FN)
+
+
+@pytest.mark.parametrize("text", [QUIRKY, QUIRKY + "\n", "v 1 2 3", "", "\n\n", "f 1 2 3\nv 1 1 1\0 junk\nv 2\0 2 2\n",
+                                  "v 1 2 3\r\n" * 50 + "f 1 2 3\r\n" * 40])
+def test_parallel_parse_edge_texts(text):
+    """No trailing newline, CRLF, empty input, NUL bytes (read as blanks), chunks smaller than a
+    line: every thread count gives the one-thread mesh."""
+    one = E.Mesh.parse_obj(text, threads=1).arrays()
+    for th in (2, 3, 5, 64):
+        assert _mesh_equal(E.Mesh.parse_obj(text, threads=th).arrays(), one), th
+
+
+def test_scene_upload_rejects_bad_sphere_and_plane_materials():
+    """atr_scene_upload validates every material index the device shading reads (mats[material])
+    before touching the context, so this runs without a GPU."""
+    L = E.lib()
+    fake_ctx = C.create_string_buffer(64)  # never dereferenced: validation fails first
+    mats = (E.atr_material * 2)()
+    for sph, pln in [([((0, 0, 0), 1.0, 2)], []), ([((0, 0, 0), 1.0, -1)], []), ([], [((0, 1, 0), 0.0, 7)]),
+                     ([], [((0, 1, 0), 0.0, -3)])]:
+        sa = (E.atr_sphere * max(1, len(sph)))(*[E.atr_sphere(E.vec3(c), r, m) for c, r, m in sph])
+        pa = (E.atr_plane * max(1, len(pln)))(*[E.atr_plane(E.vec3(n), d, m) for n, d, m in pln])
+        rc = L.atr_scene_upload(C.cast(fake_ctx, C.c_void_p), C.cast(mats, C.c_void_p), 2, None, 0,
+                                C.cast(sa, C.c_void_p), len(sph), C.cast(pa, C.c_void_p), len(pln))
+        assert rc == -1, (sph, pln, rc)
 
 
 def test_camera_matches_oracle():

@@ -1,0 +1,184 @@
+"""BASELINE.json configs C4 and C5 on the shipping kernels, and per-frame cameras.
+
+C4: Dragon 1920x1080, 64 spp, 5 bounces (app.cpp:85). C5: Dragon 3840x2160, 256 spp, 5 bounces.
+The GPU renders the whole frame; the oracle (the reference algorithm restated, one thread)
+re-renders row bands through the dragon's widest rows and its silhouette (grazing rays), and the
+band must match bit for bit: framebuffer, per-pixel ray_casts (renderer.cpp:260), primary hit
+face and t; RGB within 1e-5 relative (north star; in practice bit-exact). At full size the
+schedules must agree with each other (LANE: the reference's exact per-triangle work; PERSIST:
+the multi-bounce default; CLUSTER: the cell kernel), a size-independent property.
+Needs an MI355X (-m gpu)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from atray_amd import engine as E  # noqa: E402
+from atray_amd.assets import CENTERS, asset_path  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from tests.goldens import SEED  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+RGB_RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = E.Engine(0)
+    m = E.Mesh.load_obj(asset_path("Dragon"))
+    box = m.translate_to(m.aabb(), CENTERS["Dragon"])
+    t = E.Octree.build(m, 300)
+    e.upload([O.SKY, O.MODEL_MAT], [(m, t, box, 1)])
+    e._dragon = (m, t, box)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def oracle_scene():
+    return O.Scene(asset_path("Dragon"), center=CENTERS["Dragon"])
+
+
+def render(eng, cam, variant, with_rgb=True):
+    W, H = cam.width, cam.height
+    n = W * H
+    dev = torch.device("cuda", 0)
+    out = {"fb": torch.full((n,), 0x7F7F7F7F, dtype=torch.int32, device=dev),
+           "face": torch.full((n,), -7, dtype=torch.int32, device=dev),
+           "t": torch.zeros(n, dtype=torch.float32, device=dev),
+           "casts": torch.full((n,), -1, dtype=torch.int32, device=dev),
+           "traced": torch.zeros(1, dtype=torch.int64, device=dev)}
+    rgb = torch.zeros(3 * n, dtype=torch.float32, device=dev) if with_rgb else None
+    fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, out["fb"].data_ptr(), out["face"].data_ptr(), out["t"].data_ptr(),
+                     rgb.data_ptr() if with_rgb else None, out["casts"].data_ptr(), out["traced"].data_ptr())
+    eng.render_start(cam, [[0, 0, W - 1, H - 1]], fr, SEED, stream=torch.cuda.current_stream().cuda_stream,
+                     variant=variant)
+    rc, _ = eng.wait()
+    assert rc == 0
+    torch.cuda.synchronize()
+    if with_rgb:
+        out["rgb"] = rgb.view(H, W, 3)
+    for k in ("fb", "face", "t", "casts"):
+        out[k] = out[k].view(H, W)
+    return out
+
+
+def oracle_rows(s, ocam, y0, y1):
+    """The oracle's rows [y0, y1), one row per host thread (the ctypes calls release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, y1 - y0)) as ex:
+        parts = list(ex.map(lambda y: (s.render(ocam, SEED, y, y + 1), s.primary_hits(ocam, y, y + 1)),
+                            range(y0, y1)))
+    rgb = np.concatenate([p[0][0] for p in parts])
+    fb = np.concatenate([p[0][1] for p in parts])
+    casts = np.concatenate([p[0][2] for p in parts])
+    face = np.concatenate([p[1][0] for p in parts])
+    t = np.concatenate([p[1][1] for p in parts])
+    return rgb, fb, casts, face, t
+
+
+def check_band(o, s, ocam, y0, y1):
+    rgb, fb, casts, face, t = oracle_rows(s, ocam, y0, y1)
+    assert np.array_equal(o["fb"][y0:y1].cpu().numpy().view(np.uint32), fb), "framebuffer"
+    assert np.array_equal(o["casts"][y0:y1].cpu().numpy().view(np.uint32), casts), "ray_casts"
+    assert np.array_equal(o["face"][y0:y1].cpu().numpy().view(np.uint32), face), "hit face"
+    assert np.array_equal(o["t"][y0:y1].cpu().numpy().view(np.uint32), t.view(np.uint32)), "hit t"
+    got = o["rgb"][y0:y1].cpu().numpy()
+    if not np.array_equal(got.view(np.uint32), rgb.view(np.uint32)):
+        np.testing.assert_allclose(got, rgb, rtol=RGB_RTOL, atol=1e-7)
+    return int((face != E.MISS).sum())
+
+
+# dragon rows at 1080p: silhouette top ~312, widest ~556 (tests/golden hits_dragon_480x270 x 4)
+C4_BANDS = [(552, 560), (312, 316)]
+C5_BANDS = [(1112, 1114), (626, 627)]
+
+
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER])
+def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
+    """C4 through AUTO (= PERSIST for multi-bounce, capi.cpp auto_sched) and CLUSTER."""
+    o = render(eng, E.camera(1920, 1080, 64, 5), variant)
+    hitpx = sum(check_band(o, oracle_scene, O.Camera(1920, 1080, spp=64, bounces=5), a, b) for a, b in C4_BANDS)
+    assert hitpx > 2000  # the bands cross the dragon
+    assert int(o["traced"].item()) > 1920 * 1080 * 64
+
+
+def test_c4_schedules_agree_at_full_size(eng):
+    """Size-independent property at C4: the reference's exact work (LANE), the multi-bounce
+    default (PERSIST) and the cell kernel (CLUSTER) produce identical frames, and a re-render is
+    identical (determinism)."""
+    cam = E.camera(1920, 1080, 64, 5)
+    a = render(eng, cam, E.ATR_KERNEL_PERSIST)
+    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST):
+        b = render(eng, cam, v)
+        for k in ("fb", "casts", "face"):
+            assert torch.equal(a[k], b[k]), (v, k)
+        assert torch.equal(a["t"].view(torch.int32), b["t"].view(torch.int32))
+        assert torch.equal(a["rgb"].view(torch.int32), b["rgb"].view(torch.int32)), v
+        assert int(a["traced"].item()) == int(b["traced"].item())
+
+
+def test_c5_full_frame_band_matches_oracle(eng, oracle_scene):
+    """C5: 3840x2160, 256 spp, 5 bounces (one GPU renders the whole frame)."""
+    o = render(eng, E.camera(3840, 2160, 256, 5), E.ATR_KERNEL_AUTO)
+    hitpx = sum(check_band(o, oracle_scene, O.Camera(3840, 2160, spp=256, bounces=5), a, b) for a, b in C5_BANDS)
+    assert hitpx > 1000
+    assert int(o["traced"].item()) > 3840 * 2160 * 256
+
+
+ORBIT = [(0.1 + 0.5 * np.sin(a), 2.0, 0.5 * (1 - np.cos(a))) for a in np.linspace(0, 2 * np.pi, 7)[:-1]]
+
+
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
+                                     E.ATR_KERNEL_LANE])
+@pytest.mark.parametrize("spp,bounces", [(1, 1), (2, 3)])
+@pytest.mark.parametrize("layout", [E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED])
+def test_per_frame_cameras_equal_single_renders(eng, variant, spp, bounces, layout):
+    """atr_render_start_cameras: frame f of one launch renders cams[f] exactly as a one-camera
+    render would (the camera orbit the bench uses)."""
+    W, H = 240, 136
+    cams = [E.camera(W, H, spp, bounces, eye=e, facing=(-0.1, -0.5, -1.0)) for e in ORBIT]
+    tiles = E.make_tiles(W, H, 8)
+    n = W * H if layout == E.ATR_LAYOUT_IMAGE else E.packed_size(tiles)
+    F, stride = len(cams), n + 11
+    dev = torch.device("cuda", 0)
+    fb = torch.full((F * stride,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
+    casts = torch.full((F * stride,), -1, dtype=torch.int32, device=dev)
+    traced = torch.zeros(1, dtype=torch.int64, device=dev)
+    fr = E.atr_frame(layout, fb.data_ptr(), None, None, None, casts.data_ptr(), traced.data_ptr())
+    torch.cuda.synchronize()
+    eng.render_start_cameras(cams, tiles, fr, stride, SEED, stream=torch.cuda.current_stream().cuda_stream,
+                             variant=variant)
+    assert eng.wait()[0] == 0
+    torch.cuda.synchronize()
+    total = 0
+    for f, cam in enumerate(cams):
+        one = torch.full((n,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
+        onec = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        tr1 = torch.zeros(1, dtype=torch.int64, device=dev)
+        fr1 = E.atr_frame(layout, one.data_ptr(), None, None, None, onec.data_ptr(), tr1.data_ptr())
+        eng.render_start(cam, tiles, fr1, SEED, stream=torch.cuda.current_stream().cuda_stream, variant=variant)
+        assert eng.wait()[0] == 0
+        torch.cuda.synchronize()
+        assert torch.equal(fb[f * stride:f * stride + n], one), f
+        assert torch.equal(casts[f * stride:f * stride + n], onec), f
+        assert (fb[f * stride + n:(f + 1) * stride] == 0x7F7F7F7F).all()
+        total += int(tr1.item())
+    assert int(traced.item()) == total
+    # the frames differ (the orbit moves the eye)
+    assert not torch.equal(fb[:n], fb[stride:stride + n])
+
+
+def test_per_frame_cameras_reject_mismatched_settings(eng):
+    W, H = 64, 32
+    a, b = E.camera(W, H, 1, 1), E.camera(W, H, 2, 1)
+    fb = torch.zeros(2 * W * H, dtype=torch.int32, device="cuda")
+    fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, None, None)
+    with pytest.raises(E.AtrError):
+        eng.render_start_cameras([a, b], [[0, 0, W - 1, H - 1]], fr, W * H, SEED)
+    with pytest.raises(E.AtrError):  # more than 16 cameras in one launch
+        big = torch.zeros(17 * W * H, dtype=torch.int32, device="cuda")
+        fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, big.data_ptr(), None, None, None, None, None)
+        eng.render_start_cameras([a] * 17, [[0, 0, W - 1, H - 1]], fr, W * H, SEED)
