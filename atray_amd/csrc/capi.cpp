@@ -25,6 +25,7 @@ using namespace atr;
 
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s);
 extern "C" hipError_t atr_launch_persist(const atr::RenderParams& P, int ncu, hipStream_t s);
+extern "C" hipError_t atr_launch_traced_finish(unsigned long long* slots, unsigned long long* out, hipStream_t s);
 extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                         const uint32_t* packed, uint32_t* image, hipStream_t s);
 extern "C" hipError_t atr_wf_render(const atr::WFParams& W, int32_t nmodels, const int32_t* nnodes,
@@ -65,6 +66,18 @@ struct DevTmp {
     ~DevTmp() { if (p) (void)hipFree(p); }
 };
 
+int32_t env_int(const char* name, int32_t dflt);
+// Cell order within a tile: 1 = Z curve (default), 0 = rows (ATR_BLOCK_ORDER overrides).
+int32_t block_order() {
+    static const int32_t v = env_int("ATR_BLOCK_ORDER", 1);
+    return v;
+}
+uint64_t morton2(uint32_t x, uint32_t y) {
+    uint64_t r = 0;
+    for (int i = 0; i < 16; ++i) r |= (uint64_t((x >> i) & 1u) << (2 * i)) | (uint64_t((y >> i) & 1u) << (2 * i + 1));
+    return r;
+}
+
 // first_emit > 0: the pixels of tiles[0, first_emit) are left out (they belong to an earlier
 // launch of a progressive render) and only tiles[first_emit, ntiles) emit blocks.
 void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, std::vector<DBlock>& out,
@@ -75,8 +88,11 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     std::vector<int32_t> order;
     order.reserve(cell.size());
     std::vector<uint8_t> seen(cell.size(), 0);
+    const bool morton = block_order() == 1;
+    std::vector<int32_t> fresh;
     for (int32_t k = 0; k < ntiles; ++k) {
         atr_tile t = tiles[k];
+        fresh.clear();
         if (t.min_x < 0) t.min_x = 0;
         if (t.min_y < 0) t.min_y = 0;
         if (t.max_x > W - 1) t.max_x = W - 1;
@@ -97,9 +113,14 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
                 if (k < first_emit) { done[ci] |= m; continue; }
                 if (first_emit > 0) m &= ~done[ci];
                 if (!m) continue;
-                if (!seen[ci]) { seen[ci] = 1; order.push_back(int32_t(ci)); }
+                if (!seen[ci]) { seen[ci] = 1; fresh.push_back(int32_t(ci)); }
                 cell[ci] |= m;
             }
+        if (morton)  // the tile's cells along a Z curve: consecutive waves trace a 2D patch
+            std::stable_sort(fresh.begin(), fresh.end(), [cw](int32_t a, int32_t b) {
+                return morton2(uint32_t(a % cw), uint32_t(a / cw)) < morton2(uint32_t(b % cw), uint32_t(b / cw));
+            });
+        order.insert(order.end(), fresh.begin(), fresh.end());
     }
     out.clear();
     out.reserve(order.size());
@@ -136,6 +157,12 @@ int32_t xcd_chunk() {
     static const int32_t v = env_int("ATR_XCD_CHUNK", 16);
     return v;
 }
+// Multi-frame cell launches: rotation of each frame's block list (render.hip), 1024 = frame f
+// starts f / frames into its list; ATR_FRAME_ROTATE overrides.
+int32_t frame_rotate() {
+    static const int32_t v = std::max(0, std::min(1024, env_int("ATR_FRAME_ROTATE", 0)));
+    return v;
+}
 // PERSIST: 8x8 cells per work-queue chunk (ATR_QCHUNK overrides).
 int32_t qchunk() {
     static const int32_t v = std::max(1, env_int("ATR_QCHUNK", 16));
@@ -152,6 +179,7 @@ int32_t default_parse_threads() {
 constexpr int kSchedPersist = 8;
 constexpr int kQueueSlots = 32;             // queue-head sets in flight (ring)
 constexpr size_t kQueueBytes = 8 * 32 * 4;  // 8 heads, 128 B apart
+constexpr size_t kTraceBytes = 64 * 128;    // 64 traced-ray counters, 128 B apart (render.hip)
 
 }  // namespace
 
@@ -186,6 +214,11 @@ struct atr_ctx {
     hipEvent_t qev[kQueueSlots] = {};
     bool qused[kQueueSlots] = {};
     int qnext = 0;
+    // cell launches' traced-ray counter sets (same ring discipline, zeroed by their finish kernel)
+    void* tring = nullptr;
+    hipEvent_t tev[kQueueSlots] = {};
+    bool tused[kQueueSlots] = {};
+    int tnext = 0;
     // progressive render (atr_render_start_progressive): one launch per tile group, an event
     // after each; prog_end[g] = tiles complete once group g is
     bool prog_active = false;
@@ -398,7 +431,23 @@ int auto_sched(int32_t variant, const atr_camera& cam) {
 
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
 hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
-    if (sched != kSchedPersist) return atr_launch_render(P, sched, s);
+    if (sched != kSchedPersist) {
+        if (!P.traced_rays || P.counters) return atr_launch_render(P, sched, s);
+        // traced rays into a zeroed set of 64 spread counters, then one add to the caller's
+        const int k = c->tnext;
+        c->tnext = (k + 1) % kQueueSlots;
+        hipError_t e;
+        if (c->tused[k] && (e = hipStreamWaitEvent(s, c->tev[k], 0)) != hipSuccess) return e;
+        unsigned long long* caller = P.traced_rays;
+        P.traced_rays = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->tring) + size_t(k) * kTraceBytes);
+        e = atr_launch_render(P, sched, s);
+        if (e == hipSuccess) e = atr_launch_traced_finish(P.traced_rays, caller, s);
+        P.traced_rays = caller;
+        if (e != hipSuccess) return e;
+        if ((e = hipEventRecord(c->tev[k], s)) != hipSuccess) return e;
+        c->tused[k] = true;
+        return hipSuccess;
+    }
     if (P.nblocks <= 0) return hipSuccess;
     const int k = c->qnext;
     c->qnext = (k + 1) % kQueueSlots;
@@ -676,6 +725,9 @@ int atr_create(int device, atr_ctx** out) {
         HIPCHK(hipMalloc(&c->qring, kQueueSlots * kQueueBytes));
         HIPCHK(hipMemset(c->qring, 0, kQueueSlots * kQueueBytes));
         for (hipEvent_t& e : c->qev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipMalloc(&c->tring, kQueueSlots * kTraceBytes));
+        HIPCHK(hipMemset(c->tring, 0, kQueueSlots * kTraceBytes));
+        for (hipEvent_t& e : c->tev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         return ATR_OK;
     }();
     if (rc != ATR_OK) {
@@ -708,6 +760,9 @@ int atr_destroy(atr_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->qev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->tev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->tring) (void)hipFree(c->tring);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -1181,6 +1236,7 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
         P.nblocks = nb * nframes;
         P.frame_blocks = nb;
         P.frame_stride = frame_stride;
+        P.frame_rotate = frame_rotate();
         if (ncams > 1) {
             P.nfcam = ncams;
             for (int32_t f = 0; f < ncams; ++f) P.fcam[f] = cams[f];

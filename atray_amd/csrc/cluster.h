@@ -65,12 +65,29 @@ __device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint3
     cluster_tri_test<COUNT>(r, m.c0[k], m.c1[k], m.c2[k], k, h, ct);
 }
 
-// Cluster c (record lo = {lo.xyz, P | (n - 1)}, hi = {hi.xyz, first slot}) of the current
-// leaf: padded box tests, then the screen and the full tests of its primitives.
-template <bool COUNT>
-__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
-                                             LeafHit& h, Ctr& ct) {
-    const float ax = fabsf(r.inv.x), ay = fabsf(r.inv.y), az = fabsf(r.inv.z);
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+
+// Ray-side constants of the cluster screen, once per ray (f16 direction, its L1 norm).
+struct ScreenRay {
+    float ax, ay, az, sd;
+    h2_t dxy, dz_lo, dz_hi;
+};
+__device__ __forceinline__ ScreenRay screen_ray(const Ray& r) {
+    ScreenRay s;
+    s.ax = fabsf(r.inv.x); s.ay = fabsf(r.inv.y); s.az = fabsf(r.inv.z);
+    s.sd = fabsf(r.d.x) + fabsf(r.d.y) + fabsf(r.d.z);
+    s.dxy = h2_t{(_Float16)r.d.x, (_Float16)r.d.y};
+    const _Float16 hz = (_Float16)r.d.z;
+    s.dz_lo = h2_t{hz, (_Float16)0.0f};
+    s.dz_hi = h2_t{(_Float16)0.0f, hz};
+    return s;
+}
+
+// Cluster record lo = {lo.xyz, P | (n - 1)}, hi = {hi.xyz, q}: the two rounding-padded box
+// tests. False: no primitive inside can be accepted with t <= best. Else the det band
+// [dlo, dhi) of the primitives that still need the full test.
+__device__ __forceinline__ bool cluster_pads(const Ray& r, const ScreenRay& sr, float4_t lo, float4_t hi, float best,
+                                             float& dlo, float& dhi) {
     const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
     const float fx = fmaxf(fabsf(lo.x - r.o.x), fabsf(hi.x - r.o.x));
     const float fy = fmaxf(fabsf(lo.y - r.o.y), fabsf(hi.y - r.o.y));
@@ -86,95 +103,59 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     const float z0 = (lo.z - r.o.z) * r.inv.z, z1 = (hi.z - r.o.z) * r.inv.z;
     const float nx = fminf(x0, x1), fx1 = fmaxf(x0, x1), ny = fminf(y0, y1), fy1 = fmaxf(y0, y1),
                 nz = fminf(z0, z1), fz1 = fmaxf(z0, z1);
-    float tn = fmaxf(fmaxf(nx - gl * ax, ny - gl * ay), nz - gl * az);
-    float tf = fminf(fminf(fx1 + gl * ax, fy1 + gl * ay), fz1 + gl * az);
-    if (tn > tf || tf < 0.f || tn > h.t) return;
-    tn = fmaxf(fmaxf(nx - gt * ax, ny - gt * ay), nz - gt * az);
-    tf = fminf(fminf(fx1 + gt * ax, fy1 + gt * ay), fz1 + gt * az);
-    const bool tight = !(tn > tf || tf < 0.f || tn > h.t);
-#ifdef ATR_EXP_SKIP_LOOSE
-    if (!tight) return;  // EXPERIMENT ONLY (not exact): cost of the loose-only screens
-#endif
+    float tn = fmaxf(fmaxf(nx - gl * sr.ax, ny - gl * sr.ay), nz - gl * sr.az);
+    float tf = fminf(fminf(fx1 + gl * sr.ax, fy1 + gl * sr.ay), fz1 + gl * sr.az);
+    if (tn > tf || tf < 0.f || tn > best) return false;
+    tn = fmaxf(fmaxf(nx - gt * sr.ax, ny - gt * sr.ay), nz - gt * sr.az);
+    tf = fminf(fminf(fx1 + gt * sr.ax, fy1 + gt * sr.ay), fz1 + gt * sr.az);
+    const bool tight = !(tn > tf || tf < 0.f || tn > best);
     // screen: det estimate -q (d . p) with the cluster's quantized normals n ~ q p (p integers
     // of at most 511, f16, 96 B per cluster) and d rounded to f16, two f16 dot products per
     // primitive. |n - q p| <= q/2 per component, d's f16 rounding <= 2^-11 |d_a| + 2^-25, the
     // f32 accumulation a few eps: the estimate is within
     //   (|d.x| + |d.y| + |d.z|) q (0.51 + 511 (2^-11 + 8 eps)) + 16 eps 511 q + 2^-20 q
     // of -(d . n), which is within 16 eps |ab||ac| of the computed det; the band is widened by it.
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const float q = hi.w;
-    const float sd = fabsf(r.d.x) + fabsf(r.d.y) + fabsf(r.d.z);
-    const float mq = sd * (q * (0.51f + 511.0f * (4.8828125e-4f + 8.0f * kEps))) +
+    const float mq = sr.sd * (q * (0.51f + 511.0f * (4.8828125e-4f + 8.0f * kEps))) +
                      q * (16.0f * kEps * 511.0f + 9.5367432e-7f) + 16.0f * kEps * P;
-    const float dlo = kTol - mq, dhi = tight ? __builtin_inff() : kTau + mq;
+    dlo = kTol - mq;
+    dhi = tight ? __builtin_inff() : kTau + mq;
+    return true;
+}
+
+// Screen of 8 primitives g .. g + 7 of n: words a0, a1 hold (nx, ny) of slots g .. g + 7 as f16,
+// z the nz of slots g .. g + 7 (two per word). Bit j: slot g + j needs the full test.
+__device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float dlo, float dhi, uint4_t a0, uint4_t a1,
+                                            uint4_t z, uint32_t g, uint32_t n) {
+    const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
+    uint32_t gc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const h2_t pxy = __builtin_bit_cast(h2_t, xy[j]), pz = __builtin_bit_cast(h2_t, zz[j / 2]);
+        const float dz = __builtin_amdgcn_fdot2((j & 1) ? sr.dz_hi : sr.dz_lo, pz, 0.0f, false);
+        const float e = __builtin_amdgcn_fdot2(sr.dxy, pxy, dz, false) * nq;
+        if (g + j < n && e >= dlo && e < dhi) gc |= 1u << j;
+    }
+    return gc;
+}
+
+// Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and
+// the full tests of its primitives.
+template <bool COUNT>
+__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
+                                             LeafHit& h, Ctr& ct) {
+    const ScreenRay sr = screen_ray(r);
+    float dlo, dhi;
+    if (!cluster_pads(r, sr, lo, hi, h.t, dlo, dhi)) return;
     const uint32_t first = kMaxClusterSize * c;
     const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u;
     if constexpr (COUNT) ct.screen += n;
-    const h2 dxy = {(_Float16)r.d.x, (_Float16)r.d.y};
-    const _Float16 hz = (_Float16)r.d.z;
-    const h2 dz_lo = {hz, (_Float16)0.0f}, dz_hi = {(_Float16)0.0f, hz};
     const uint4_t* nb = m.cnrm + kClusterBlock * size_t(c);
-    const float nq = -q;
+    const float nq = -hi.w;
     uint32_t cand = 0;
-#ifdef ATR_SPHERE
-    // Sphere filter (opt-in, -DATR_SPHERE; measured slower: 3x fewer full tests but 1.00 ->
-    // 1.14 ms on c3): a candidate is fully tested only if the ray's line passes within its
-    // bounding sphere grown by the same rounding pad as the box (g(kTau) when the screen proves
-    // det >= kTau, else g(kTol)): any hit the test accepts has the true line within that pad of
-    // the triangle (§ Rounding bound above). Centre = lo + u * ext / 255 per axis, radius =
-    // r_q * emax / 255 (host-rounded to hold the triangle around the decoded centre); the f32
-    // decode and the |w x d| evaluation add at most 8 eps (W + |box|).
-    const uint4_t* sp = nb + 6;
-    const float sx = ex * (1.0f / 255.0f), sy = ey * (1.0f / 255.0f), sz = ez * (1.0f / 255.0f);
-    const float sr = fmaxf(ex, fmaxf(ey, ez)) * (1.0f / 255.0f) * 1.000001f;
-    const float cabs = fmaxf(fmaxf(fmaxf(fabsf(lo.x), fabsf(hi.x)), fmaxf(fabsf(lo.y), fabsf(hi.y))),
-                             fmaxf(fabsf(lo.z), fabsf(hi.z)));
-    const float slack = 8.0f * kEps * (W + 2.0f * cabs) + 1e-30f;
-    const float addl = gl * 1.000001f + slack, addt = gt * 1.000001f + slack;
-    const float tq = kTau + mq;
-#endif
-    for (uint32_t g = 0; g < n; g += 8) {  // eight primitives per step: (nx, ny) x 8, nz x 8
-        const uint4_t a0 = nb[g / 4], a1 = nb[g / 4 + 1], z = nb[4 + g / 8];
-#ifdef ATR_SPHERE
-        const uint4_t w0 = sp[g / 4], w1 = sp[g / 4 + 1];
-        uint32_t gt8 = 0;  // candidates whose det is proven >= kTau
-#endif
-        const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
-        uint32_t gc = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const h2 pxy = __builtin_bit_cast(h2, xy[j]), pz = __builtin_bit_cast(h2, zz[j / 2]);
-            const float dz = __builtin_amdgcn_fdot2((j & 1) ? dz_hi : dz_lo, pz, 0.0f, false);
-            const float e = __builtin_amdgcn_fdot2(dxy, pxy, dz, false) * nq;
-            if (g + j < n && e >= dlo && e < dhi) gc |= 1u << j;
-#ifdef ATR_SPHERE
-            if (e >= tq) gt8 |= 1u << j;
-#endif
-        }
-#ifdef ATR_SPHERE
-        uint32_t gm = gc;
-        gc = 0;
-        while (gm) {
-            const int k = __builtin_ctz(gm);
-            gm &= gm - 1;
-            const uint32_t wa = (k & 1) ? ((k & 4) ? w1.y : w0.y) : ((k & 4) ? w1.x : w0.x);
-            const uint32_t wb = (k & 1) ? ((k & 4) ? w1.w : w0.w) : ((k & 4) ? w1.z : w0.z);
-            const uint32_t w = (k & 2) ? wb : wa;
-            const float wx = fmaf(float(w & 0xFFu), sx, lo.x) - r.o.x;
-            const float wy = fmaf(float((w >> 8) & 0xFFu), sy, lo.y) - r.o.y;
-            const float wz = fmaf(float((w >> 16) & 0xFFu), sz, lo.z) - r.o.z;
-            const float px = wy * r.d.z - wz * r.d.y, py = wz * r.d.x - wx * r.d.z, pz = wx * r.d.y - wy * r.d.x;
-            const float R = fmaf(float(w >> 24), sr, ((gt8 >> k) & 1u) ? addt : addl);
-            if (px * px + py * py + pz * pz <= R * R * 1.000001f) gc |= 1u << k;
-        }
-#endif
-        cand |= gc << g;
-    }
-#ifdef ATR_EXP_NO_TRI
-    if (cand) h.improved |= (cand == 0x12345u);  // EXPERIMENT ONLY (not exact): no full tests
-    cand = 0;
-#endif
+    for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
+        cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8], g, n) << g;
     while (cand) {  // full tests of the candidates in slot order, two primitives' loads in flight
         const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
         cand &= cand - 1;

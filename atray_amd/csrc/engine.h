@@ -185,6 +185,7 @@ struct RenderParams {
     int32_t qchunk;     // PERSIST: 8x8 cells per queue chunk
     int32_t frame_blocks;  // > 0: nblocks = frames x frame_blocks, one launch renders every frame
     int64_t frame_stride;  // output elements between consecutive frames (rgb: 3 x this)
+    int32_t frame_rotate;  // frame f's blocks start f / frames x frame_rotate / 1024 into its list
     int32_t nfcam;         // > 0: frame f renders with fcam[f] instead of cam (same size/spp/bounces)
     atr_camera fcam[kMaxFrameCams];
 };

@@ -115,20 +115,31 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
         float bd = -__builtin_inff();
         int32_t bi = -1;
         bool more = true;
+        // The sorted leaves of a pass wait in LDS (a lane-private column, 64 B per lane, 16 KB
+        // per 4-wave workgroup) while they are scanned: the 16 registers of the leaf buffer are
+        // live only during the pass and the scan's registers only during the scan, so the
+        // kernel's peak is the larger of the two, not their sum (no scratch spills at 5
+        // waves/SIMD).
+        __shared__ float s_lbd[4][K][64];
+        __shared__ int32_t s_lbl[4][K][64];
+        const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
         while (more) {
-            LeafBuf<K> lb;
-            const int32_t n = traverse_pass<K, COUNT>(r, tab, lb, bd, bi, ct);
+            int32_t n;
+            {
+                LeafBuf<K> lb;
+                n = traverse_pass<K, COUNT>(r, tab, lb, bd, bi, ct);
+#pragma unroll
+                for (int j = 0; j < K; ++j) { s_lbd[w][j][ln] = lb.d[j]; s_lbl[w][j][ln] = lb.leaf[j]; }
+            }
             if (n < 0) { err = 1; break; }
-            int32_t nb = n < K ? n : K;
+            const int32_t nb = n < K ? n : K;
             more = n > K;
             bool hit = false;
-            while (nb > 0) {
-                const int32_t leaf = lb.leaf[0];
-                bd = lb.d[0];
-                bi = lb.leaf[0];
+            for (int32_t j = 0; j < nb; ++j) {
+                const int32_t leaf = s_lbl[w][j][ln];
+                bd = s_lbd[w][j][ln];
+                bi = leaf;
                 if (scan(leaf)) { hit = true; break; }
-                lb_pop<K>(lb);
-                --nb;
             }
             if (hit) break;
         }
@@ -503,8 +514,14 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     // neighbouring workgroups trace the same cells' rays)
     const int32_t nf = P.frame_blocks > 0 ? P.nblocks / P.frame_blocks : 1;
     const int32_t fidx = b % nf;
+    // frame f's block list rotated by f / nf x frame_rotate / 1024 of the frame: the frames' slow
+    // regions reach the dispatcher at different times instead of all together
+    int32_t bi = b / nf;
+    if (P.frame_rotate && nf > 1)
+        bi = int32_t((int64_t(bi) + int64_t(P.frame_blocks) * fidx * P.frame_rotate / (1024 * int64_t(nf))) %
+                     P.frame_blocks);
     DBlock blk;
-    if (in_range) blk = P.blocks[b / nf];
+    if (in_range) blk = P.blocks[bi];
     else { blk.x0 = 0; blk.y0 = 0; blk.mask_lo = 0; blk.mask_hi = 0; blk.out_base = 0; }
     const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
     const bool active = (mask >> lane) & 1;
@@ -574,7 +591,9 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         uint32_t t = traced;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-        if (lane == 0 && t) atomicAdd(P.traced_rays, (unsigned long long)t);
+        // 64 counters on separate 128-B lines (atr_launch_traced_finish adds them up): one
+        // address taking every wave's add serializes ~0.1 ms per frame at the L2
+        if (lane == 0 && t) atomicAdd(P.traced_rays + 16 * (b & 63), (unsigned long long)t);
     }
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
     if (P.block_cost && lane == 0 && in_range) P.block_cost[b] = clock64() - clk0;
@@ -628,6 +647,17 @@ template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 4>(RenderP
 template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_CLUSTER_K4, false, true, 8>(RenderParams);
+
+// Sum the 64 traced-ray counters of a cell launch into the caller's accumulator and clear them.
+__global__ __launch_bounds__(64) void traced_finish_kernel(unsigned long long* __restrict__ slots,
+                                                          unsigned long long* __restrict__ out) {
+    const int lane = threadIdx.x;
+    unsigned long long v = slots[16 * lane];
+    slots[16 * lane] = 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0 && v) atomicAdd(out, v);
+}
 
 __global__ __launch_bounds__(256) void unpack_kernel(const DBlock* __restrict__ blocks, int32_t nblocks,
                                                      int32_t width, const uint32_t* __restrict__ packed,
@@ -722,6 +752,11 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
             break;
         default: launch_sched<atr::SCHED_LANE>(P, count, prim, s); break;
     }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t atr_launch_traced_finish(unsigned long long* slots, unsigned long long* out, hipStream_t s) {
+    hipLaunchKernelGGL(atr::traced_finish_kernel, dim3(1), dim3(64), 0, s, slots, out);
     return hipGetLastError();
 }
 

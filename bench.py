@@ -216,7 +216,7 @@ def main():
     ap.add_argument("--no-prep", action="store_true", help="skip the device octree build timing")
     ap.add_argument("--no-orbit", action="store_true", help="every frame from the app camera")
     ap.add_argument("--streams", type=int, default=2, help="launches in flight (one HIP stream each)")
-    ap.add_argument("--frames-per-launch", type=int, default=8,
+    ap.add_argument("--frames-per-launch", type=int, default=4,
                     help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
@@ -416,6 +416,8 @@ def run(args):
         """Launch j's gather done (its stream waits on it); rank 0 scatters every rank's packed
         frames into that slot's images, on the launch's stream."""
         q, work = pending.pop(j)
+        if world == 1:
+            return
         with torch.cuda.stream(streams[q]):
             if work is not None:
                 work.wait()
