@@ -417,6 +417,7 @@ int sched_of(int32_t variant) {
         case ATR_KERNEL_TILE8: return 3;
         case ATR_KERNEL_CLUSTER: return 4;
         case ATR_KERNEL_PERSIST: return kSchedPersist;
+        case ATR_KERNEL_FLAT: return 6;
         case ATR_KERNEL_AUTO: return 4;  // see auto_sched
         default: return variant >= 16 ? variant : 0;
     }

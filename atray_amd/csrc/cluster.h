@@ -156,6 +156,13 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
         cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8], g, n) << g;
+#ifdef ATR_SINGLE_CAND
+    while (cand) {
+        const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
+        cand &= cand - 1;
+        cluster_tri_test<COUNT>(r, m.c0[ka], m.c1[ka], m.c2[ka], ka, h, ct);
+    }
+#endif
     while (cand) {  // full tests of the candidates in slot order, two primitives' loads in flight
         const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
         cand &= cand - 1;

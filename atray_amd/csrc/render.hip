@@ -238,6 +238,166 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
     }
 }
 
+// ------------------------------------------------------------------ FLAT schedule
+// The clustered scan with the wavefront's (ray, cluster) work flattened over its lanes
+// (DESIGN.md §4e). In the lane-private scan (CLUSTER) every loop level diverges -- rays visit
+// different numbers of leaves, their current leaves hold 1-20 clusters, the clusters pass the
+// padded box or not -- and the wavefront executes the union: a slow 8x8 cell issued ~150 k VALU
+// instructions where its rays' own work is ~7x less. Here each lane still owns a ray's query
+// (traversal passes, its sorted leaves, the first-improving-leaf rule), but the clusters of all
+// rays' current leaves are dealt to the 64 lanes in rounds: a round's 64 lanes each take one
+// (ray, cluster) item and run the same cluster test on the owner's ray (read from the owner lane
+// with a lane shuffle). Results merge per owner in LDS as the minimum (t, leaf rank) -- the
+// first primitive in leaf order with the smallest t (kd_tree.cpp:440-456) -- so every output is
+// CLUSTER's, bit for bit.
+__device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src); }
+
+template <bool COUNT>
+__device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
+                                                  Ctr& ct) {
+    constexpr int K = kLeafBuf;
+    constexpr unsigned long long kInit = (static_cast<unsigned long long>(0x7F7FFFFFu) << 32) | 0xFFFFFFFFull;
+    __shared__ float s_lbd[4][K][64];
+    __shared__ int32_t s_lbl[4][K][64];
+    __shared__ unsigned long long s_key[4][64];
+    __shared__ uint32_t s_slot[4][64];
+    __shared__ float s_u[4][64], s_v[4][64];
+    __shared__ int32_t s_mark[4][64];
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    h.t = kMaxFloat;
+    h.face = 0;
+    h.u = h.v = 0.f;
+    bool done = true, need = false, more = false;
+    int32_t j = 0, nb = 0, bi = -1;
+    float bd = -__builtin_inff();
+    if (active) {
+        const NodeBox root = load_node(m.nodes, 0);
+        if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
+        if (box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) {  // kd_tree.cpp:339
+            done = false;
+            if (root.children == 0) {  // :344-361: the root leaf (discovery rank 0) alone
+                s_lbl[w][0][ln] = 0;
+                s_lbd[w][0][ln] = 0.f;
+                nb = 1;
+            } else {
+                need = true;
+            }
+        }
+    }
+    uint32_t res_slot = 0xFFFFFFFFu;
+    float res_t = kMaxFloat, res_u = 0.f, res_v = 0.f;
+    for (;;) {
+        if (need) {  // one DFS pass (kd_tree.cpp:363-435); its sorted leaves wait in LDS
+            int32_t n;
+            {
+                LeafBuf<K> lb;
+                n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+#pragma unroll
+                for (int q = 0; q < K; ++q) { s_lbd[w][q][ln] = lb.d[q]; s_lbl[w][q][ln] = lb.leaf[q]; }
+            }
+            need = false;
+            j = 0;
+            if (n < 0) { err = 1; done = true; }
+            else { nb = n < K ? n : K; more = n > K; if (nb == 0) done = true; }
+        }
+        if (__ballot(!done) == 0) break;
+        // every live ray's current leaf: its clusters are this step's items
+        int32_t leaf = -1;
+        uint32_t cf = 0, cn = 0;
+        if (!done) {
+            leaf = s_lbl[w][j][ln];
+            const uint2_t cr = load_range(m.cl_range, leaf);
+            cf = cr.x;
+            cn = cr.y;
+            if constexpr (COUNT) { ct.leaf += 1; ct.cbox += cn; }
+        }
+        uint32_t incl = cn;  // inclusive prefix sum over the lanes
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = uint32_t(__shfl_up(int(incl), off));
+            if (ln >= off) incl += t;
+        }
+        const uint32_t excl = incl - cn;
+        const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
+        s_key[w][ln] = kInit;
+        int32_t carry = -1;
+        for (uint32_t base = 0; base < total; base += 64) {  // rounds of 64 items, wave-uniform
+            s_mark[w][ln] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (cn > 0 && excl >= base && excl < base + 64u) s_mark[w][excl - base] = ln;
+            __builtin_amdgcn_wave_barrier();
+            int32_t own = s_mark[w][ln];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {  // latest owner starting at or before this lane
+                const int32_t t = __shfl_up(own, off);
+                if (ln >= off && t > own) own = t;
+            }
+            if (own < 0) own = carry;
+            carry = __builtin_amdgcn_readlane(own, 63);
+            const uint32_t k = base + uint32_t(ln);
+            const bool valid = k < total;
+            const int32_t src = valid ? own : ln;
+            Ray q;  // the owner's ray
+            q.o = mk(shfl_f(r.o.x, src), shfl_f(r.o.y, src), shfl_f(r.o.z, src));
+            q.d = mk(shfl_f(r.d.x, src), shfl_f(r.d.y, src), shfl_f(r.d.z, src));
+            q.inv = mk(shfl_f(r.inv.x, src), shfl_f(r.inv.y, src), shfl_f(r.inv.z, src));
+            q.s0 = q.inv.x < 0;
+            q.s1 = q.inv.y < 0;
+            q.s2 = q.inv.z < 0;
+            const uint32_t c = uint32_t(__shfl(int(cf), src)) + (k - uint32_t(__shfl(int(excl), src)));
+            unsigned long long mine = kInit;
+            LeafHit lh;
+            lh.improved = false;
+            if (valid) {
+                const unsigned long long cur = s_key[w][own];
+                // the owner's best in this leaf so far: pruning bound, and equal t then loses only
+                // to a smaller leaf rank (a fresh leaf starts from MAX_FLOAT, strict <)
+                lh.t = __uint_as_float(uint32_t(cur >> 32));
+                lh.rank = cur == kInit ? -1 : int32_t(uint32_t(cur));
+                lh.slot = 0xFFFFFFFFu;
+                lh.u = lh.v = 0.f;
+                const float4_t lo = m.clus[kClusterBlock * size_t(c)], hi = m.clus[kClusterBlock * size_t(c) + 1];
+                cluster_step<COUNT>(q, m, c, lo, hi, lh, ct);
+                if (lh.improved) {
+                    mine = (static_cast<unsigned long long>(__float_as_uint(lh.t)) << 32) | uint32_t(lh.rank);
+                    atomicMin(&s_key[w][own], mine);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lh.improved && s_key[w][own] == mine) {  // the round's winner for this owner
+                s_slot[w][own] = lh.slot;
+                s_u[w][own] = lh.u;
+                s_v[w][own] = lh.v;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
+            const unsigned long long key = s_key[w][ln];
+            if (key != kInit) {
+                res_t = __uint_as_float(uint32_t(key >> 32));
+                res_slot = s_slot[w][ln];
+                res_u = s_u[w][ln];
+                res_v = s_v[w][ln];
+                done = true;
+            } else {
+                bd = s_lbd[w][j][ln];
+                bi = leaf;
+                if (++j >= nb) {
+                    if (more) need = true;
+                    else done = true;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (res_slot != 0xFFFFFFFFu) {
+        h.t = res_t;
+        h.u = res_u;
+        h.v = res_v;
+        h.face = m.cface[res_slot];
+    }
+}
+
 // ------------------------------------------------------------------ TILE schedule
 // The NW waves of a workgroup (NW 8x8 cells) cooperate on leaf scans. Each round elects ONE
 // leaf that some ray of the workgroup wants next (at any position of its own sorted list),
@@ -384,9 +544,12 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 }
 
 // ------------------------------------------------------------------ get_intersection_data
-enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5 };
+enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5,
+       SCHED_FLAT = 6 };
 constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
-constexpr bool sched_coop(int sc) { return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4; }  // lanes must stay in lockstep loops
+constexpr bool sched_coop(int sc) {  // lanes must stay in lockstep loops (workgroup-wide)
+    return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && sc != SCHED_FLAT;
+}
 
 template <int SCHED, bool COUNT>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
@@ -402,6 +565,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
             Hit h;
             if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
+            else if constexpr (SCHED == SCHED_FLAT) tree_closest_flat<COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
@@ -446,7 +610,7 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
     // cooperate on leaf scans inside intersect_scene.
     for (i = 0; ; ++i) {
         const bool go = live && i < bounce_limit;
-        if constexpr (SCHED == SCHED_WAVE) { if (__ballot(go) == 0) break; }
+        if constexpr (SCHED == SCHED_WAVE || SCHED == SCHED_FLAT) { if (__ballot(go) == 0) break; }
         else if constexpr (sched_coop(SCHED)) { if (!__syncthreads_or(go)) break; }
         else if (!go) break;
         Isect id;
@@ -635,6 +799,10 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
 #define ATR_INST(SC, C, PR) template __global__ void render_kernel<SC, C, PR>(RenderParams);
 #define ATR_INST4(SC) ATR_INST(SC, false, false) ATR_INST(SC, true, false) ATR_INST(SC, false, true) ATR_INST(SC, true, true)
 ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCHED_TILE8) ATR_INST4(SCHED_CLUSTER)
+ATR_INST4(SCHED_FLAT)
+template __global__ void render_kernel<SCHED_FLAT, false, true, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT, false, true, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT, false, false, 5>(RenderParams);
 #undef ATR_INST4
 #undef ATR_INST
 template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
@@ -717,6 +885,14 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);
+    if (sched >= 64) {  // FLAT at 64 + n waves/SIMD (diagnostic)
+        const int o = sched - 64;
+        if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 5>), g, b, 0, s, P);
+        else if (!count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
+        else if (!count && o == 6 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 6>), g, b, 0, s, P);
+        else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
+        return hipGetLastError();
+    }
     if (sched >= 48) {  // CLUSTER with a 4-entry leaf buffer at 48 + n waves/SIMD (diagnostic)
         const int o = sched - 48;
         if (!prim || count) return hipErrorInvalidValue;
@@ -744,6 +920,7 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     }
     switch (sched) {
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
+        case 6: launch_sched<atr::SCHED_FLAT>(P, count, prim, s); break;
         case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;
         case 3: launch_sched<atr::SCHED_TILE8>(P, count, prim, s); break;
         case 4:

@@ -23,6 +23,7 @@ ATR_KERNEL_AUTO, ATR_KERNEL_LANE, ATR_KERNEL_WAVE, ATR_KERNEL_TILE, ATR_KERNEL_T
 ATR_KERNEL_WAVEFRONT = 5
 ATR_KERNEL_CLUSTER = 6
 ATR_KERNEL_PERSIST = 7
+ATR_KERNEL_FLAT = 8
 MISS = 0xFFFFFFFF
 MAX_FLOAT = np.float32(3.402823466e38)
 

@@ -208,7 +208,7 @@ def main():
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps"])
+    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps", "flat"])
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,7 +340,7 @@ def run(args):
     variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE,
                "tile": E.ATR_KERNEL_TILE, "tile8": E.ATR_KERNEL_TILE8,
                "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
-               "ps": E.ATR_KERNEL_PERSIST}[args.variant]
+               "ps": E.ATR_KERNEL_PERSIST, "flat": E.ATR_KERNEL_FLAT}[args.variant]
     # ---- scene prep (untimed for Mrays/s; reported under "prep")
     prep = {}
     path = asset_path(asset)
@@ -543,7 +543,7 @@ def run(args):
                                "camera": "app", "rays": n1}
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
-        clustered = args.variant in ("auto", "cl", "ps")
+        clustered = args.variant in ("auto", "cl", "ps", "flat")
         bpr = cluster_bytes_per_ray(live_ctr) if clustered else algorithmic_bytes_per_ray(live_ctr)
         achieved = bpr * n1 / (kern_ms * 1e-3) / 1e9
         roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),

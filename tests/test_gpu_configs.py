@@ -96,7 +96,7 @@ C4_BANDS = [(552, 560), (312, 316)]
 C5_BANDS = [(1112, 1114), (626, 627)]
 
 
-@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER])
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_FLAT])
 def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
     """C4 through AUTO (= PERSIST for multi-bounce, capi.cpp auto_sched) and CLUSTER."""
     o = render(eng, E.camera(1920, 1080, 64, 5), variant)
@@ -111,7 +111,7 @@ def test_c4_schedules_agree_at_full_size(eng):
     identical (determinism)."""
     cam = E.camera(1920, 1080, 64, 5)
     a = render(eng, cam, E.ATR_KERNEL_PERSIST)
-    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST):
+    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT):
         b = render(eng, cam, v)
         for k in ("fb", "casts", "face"):
             assert torch.equal(a[k], b[k]), (v, k)
@@ -132,7 +132,7 @@ ORBIT = [(0.1 + 0.5 * np.sin(a), 2.0, 0.5 * (1 - np.cos(a))) for a in np.linspac
 
 
 @pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
-                                     E.ATR_KERNEL_LANE])
+                                     E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT])
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (2, 3)])
 @pytest.mark.parametrize("layout", [E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED])
 def test_per_frame_cameras_equal_single_renders(eng, variant, spp, bounces, layout):
