@@ -423,11 +423,12 @@ int sched_of(int32_t variant) {
     }
 }
 
-// AUTO: the fastest exact schedule for the camera (DESIGN.md §4c, measured): primary-only renders
-// (bounce_limit 1, no AA) on 8x8 cells (CLUSTER), multi-bounce paths on PERSIST.
+// AUTO: the fastest exact schedule for the camera (DESIGN.md §4, measured): primary-only renders
+// (bounce_limit 1, no AA) on lane-private 8x8 cells (CLUSTER, coherent rays), everything else on
+// the flattened cluster rounds (FLAT: incoherent secondary rays diverge at every loop level).
 int auto_sched(int32_t variant, const atr_camera& cam) {
     if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
-    return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_CLUSTER) : kSchedPersist;
+    return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_CLUSTER) : sched_of(ATR_KERNEL_FLAT);
 }
 
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.

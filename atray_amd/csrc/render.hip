@@ -803,6 +803,8 @@ ATR_INST4(SCHED_FLAT)
 template __global__ void render_kernel<SCHED_FLAT, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, false, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT, false, false, 3>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT, false, false, 2>(RenderParams);
 #undef ATR_INST4
 #undef ATR_INST
 template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
@@ -890,6 +892,8 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
         if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 5>), g, b, 0, s, P);
         else if (!count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
         else if (!count && o == 6 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 6>), g, b, 0, s, P);
+        else if (!count && o == 3 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 3>), g, b, 0, s, P);
+        else if (!count && o == 2 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 2>), g, b, 0, s, P);
         else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
         return hipGetLastError();
     }

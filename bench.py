@@ -209,6 +209,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps", "flat"])
+    ap.add_argument("--variant-code", type=int, default=-1,
+                    help="diagnostic: raw kernel code passed to the engine (overrides --variant's kernel)")
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -341,6 +343,8 @@ def run(args):
                "tile": E.ATR_KERNEL_TILE, "tile8": E.ATR_KERNEL_TILE8,
                "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
                "ps": E.ATR_KERNEL_PERSIST, "flat": E.ATR_KERNEL_FLAT}[args.variant]
+    if args.variant_code >= 0:
+        variant = args.variant_code
     # ---- scene prep (untimed for Mrays/s; reported under "prep")
     prep = {}
     path = asset_path(asset)
@@ -557,8 +561,8 @@ def run(args):
             rbpr = algorithmic_bytes_per_ray(ctr)
             roof["ref_bytes_per_ray"] = round(rbpr, 1)
             roof["ref_equivalent_GBs"] = round(rbpr * n1 / (kern_ms * 1e-3) / 1e9, 1)
-        prim = bounces == 1  # AUTO: CLUSTER cells for primary-only renders, PERSIST otherwise
-        kname = "persist_kernel" if args.variant == "ps" or (args.variant == "auto" and not prim) else "render_kernel"
+        # AUTO: CLUSTER cells for primary-only renders, FLAT cells otherwise (both render_kernel)
+        kname = "persist_kernel" if args.variant == "ps" else "render_kernel"
         roof["kernel"] = kname
         if world == 1 and not args.no_pmc:
             traffic, why = pmc_traffic(args, kname)

@@ -1,11 +1,8 @@
 export TMPDIR=/tmp
-O=gpurun_out/r2e
+O=gpurun_out/r2g
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -2 $O/pytest.log
-timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 --no-pmc --no-cpu-baseline --no-prep > $O/bench_c4.log 2>&1 || { tail $O/bench_c4.log; exit 1; }
-grep '^{' $O/bench_c4.log | cut -c1-600
-timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 --no-pmc --no-cpu-baseline --no-prep --variant cl > $O/bench_c4_cl.log 2>&1 || exit 1
-grep '^{' $O/bench_c4_cl.log | cut -c1-400
-timeout -k 10 400 python bench.py --config c5 --steps 1 --warmup 1 --frames-per-launch 1 --streams 1 --no-pmc --no-cpu-baseline --no-prep > $O/bench_c5.log 2>&1 || { tail $O/bench_c5.log; exit 1; }
-grep '^{' $O/bench_c5.log | cut -c1-600
+for cfg in "c4 67 4" "c4 68 4" "c4 66 4" "c5 67 1" "c5 68 1"; do
+  set -- $cfg
+  timeout -k 10 300 python bench.py --config $1 --variant flat --variant-code $2 --frames-per-launch $3 --steps 2 --warmup 1 --no-pmc --no-cpu-baseline --no-prep > $O/b_$1_$2_$3.log 2>&1 || { tail -3 $O/b_$1_$2_$3.log; exit 1; }
+  python -c "import json; d=[json.loads(l) for l in open('$O/b_$1_$2_$3.log') if l.startswith('{')][-1]; print('$cfg', d['value'], d['ms_per_step'], d['single_frame']['kernel_ms'])"
+done

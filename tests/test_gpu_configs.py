@@ -5,8 +5,9 @@ The GPU renders the whole frame; the oracle (the reference algorithm restated, o
 re-renders row bands through the dragon's widest rows and its silhouette (grazing rays), and the
 band must match bit for bit: framebuffer, per-pixel ray_casts (renderer.cpp:260), primary hit
 face and t; RGB within 1e-5 relative (north star; in practice bit-exact). At full size the
-schedules must agree with each other (LANE: the reference's exact per-triangle work; PERSIST:
-the multi-bounce default; CLUSTER: the cell kernel), a size-independent property.
+schedules must agree with each other (LANE: the reference's exact per-triangle work; FLAT: the
+multi-bounce default; CLUSTER: the primary-ray default; PERSIST: persistent lanes), a
+size-independent property.
 Needs an MI355X (-m gpu)."""
 import numpy as np
 import pytest
@@ -96,9 +97,9 @@ C4_BANDS = [(552, 560), (312, 316)]
 C5_BANDS = [(1112, 1114), (626, 627)]
 
 
-@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_FLAT])
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST])
 def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
-    """C4 through AUTO (= PERSIST for multi-bounce, capi.cpp auto_sched) and CLUSTER."""
+    """C4 through AUTO (= FLAT for multi-bounce, capi.cpp auto_sched), CLUSTER and FLAT."""
     o = render(eng, E.camera(1920, 1080, 64, 5), variant)
     hitpx = sum(check_band(o, oracle_scene, O.Camera(1920, 1080, spp=64, bounces=5), a, b) for a, b in C4_BANDS)
     assert hitpx > 2000  # the bands cross the dragon
@@ -107,8 +108,8 @@ def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
 
 def test_c4_schedules_agree_at_full_size(eng):
     """Size-independent property at C4: the reference's exact work (LANE), the multi-bounce
-    default (PERSIST) and the cell kernel (CLUSTER) produce identical frames, and a re-render is
-    identical (determinism)."""
+    default (FLAT), the cell kernel (CLUSTER) and the persistent lanes (PERSIST) produce identical
+    frames, and a re-render is identical (determinism)."""
     cam = E.camera(1920, 1080, 64, 5)
     a = render(eng, cam, E.ATR_KERNEL_PERSIST)
     for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT):
