@@ -469,7 +469,7 @@ hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) 
 
 extern "C" {
 
-const char* atr_version(void) { return "atray-mi355x 0.1 (gfx950)"; }
+const char* atr_version(void) { return "atray-mi355x 0.2 (gfx950)"; }
 
 // ------------------------------------------------------------------ host prerequisites
 int atr_mesh_parse_obj_threaded(const char* text, size_t len, int32_t threads, atr_mesh** out) {
