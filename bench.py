@@ -218,8 +218,9 @@ def main():
     ap.add_argument("--no-prep", action="store_true", help="skip the device octree build timing")
     ap.add_argument("--no-orbit", action="store_true", help="every frame from the app camera")
     ap.add_argument("--streams", type=int, default=2, help="launches in flight (one HIP stream each)")
-    ap.add_argument("--frames-per-launch", type=int, default=4,
-                    help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch")
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch; "
+                         "0 = 4 x ranks (each rank's launch keeps about 4 full frames of work)")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
@@ -229,13 +230,15 @@ def main():
     ap.add_argument("--selftest", action="store_true",
                     help="CPU only: synthetic fill instead of the render kernel (launch/plan/gather test)")
     args = ap.parse_args()
-    args.frames_per_launch = max(1, min(16, args.frames_per_launch))
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.frames_per_launch <= 0:
+        args.frames_per_launch = 4 * world
+    args.frames_per_launch = max(1, min(16, args.frames_per_launch))
     if args.selftest:
         return selftest(args)
     return run(args)

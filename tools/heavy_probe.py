@@ -13,6 +13,7 @@ from atray_amd.assets import CENTERS, asset_path  # noqa: E402
 
 W, H = 1920, 1080
 SEED = 0x853C49E6748FEA9B
+VARIANT = int(os.environ.get("VARIANT", str(E.ATR_KERNEL_CLUSTER)))
 mesh = E.Mesh.load_obj(asset_path("Dragon"))
 box = mesh.translate_to(mesh.aabb(), CENTERS["Dragon"])
 tree = E.Octree.build(mesh, 300)
@@ -42,11 +43,11 @@ for bi in order[:4]:
         for _ in range(5):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
-            eng.render_start_frames(cam, tile, frp, n, 64, SEED, stream=s.cuda_stream, variant=E.ATR_KERNEL_CLUSTER)
+            eng.render_start_frames(cam, tile, frp, n, 64, SEED, stream=s.cuda_stream, variant=VARIANT)
             b.record(s)
             torch.cuda.synchronize()
             ms.append(a.elapsed_time(b))
         res[f"alone_x{n}_us"] = round(float(np.median(ms[1:])) * 1e3, 1)
-    c = eng.counters(cam, tile, SEED, E.ATR_KERNEL_CLUSTER)
+    c = eng.counters(cam, tile, SEED, VARIANT)
     res["per_ray"] = {k: round(c[k] / 64, 1) for k in ("n_box", "box_all", "n_leaf", "cluster_boxes", "screened", "n_tri", "passes")}
     print(json.dumps(res), flush=True)
