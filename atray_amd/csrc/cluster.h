@@ -142,7 +142,7 @@ __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float
 
 // Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and
 // the full tests of its primitives.
-template <bool COUNT>
+template <bool COUNT, bool PAIR = false>
 __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
                                              LeafHit& h, Ctr& ct) {
     const ScreenRay sr = screen_ray(r);
@@ -156,27 +156,30 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
         cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8], g, n) << g;
-#ifdef ATR_SINGLE_CAND
-    while (cand) {
-        const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
-        cand &= cand - 1;
-        cluster_tri_test<COUNT>(r, m.c0[ka], m.c1[ka], m.c2[ka], ka, h, ct);
-    }
-#endif
-    while (cand) {  // full tests of the candidates in slot order, two primitives' loads in flight
-        const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
-        cand &= cand - 1;
-        const float4_t a0 = m.c0[ka], a1 = m.c1[ka];
-        const c2_t a2 = m.c2[ka];
-        if (cand) {
-            const uint32_t kb = first + uint32_t(__builtin_ctz(cand));
+    if constexpr (!PAIR) {
+        // one at a time: the lane-private CLUSTER kernel's peak stays at 94 VGPRs (no scratch at
+        // 5 waves/SIMD); two in flight measured slower there
+        while (cand) {
+            const uint32_t k = first + uint32_t(__builtin_ctz(cand));
             cand &= cand - 1;
-            const float4_t b0 = m.c0[kb], b1 = m.c1[kb];
-            const c2_t b2 = m.c2[kb];
-            cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
-            cluster_tri_test<COUNT>(r, b0, b1, b2, kb, h, ct);
-        } else {
-            cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
+            cluster_tri_test<COUNT>(r, m.c0[k], m.c1[k], m.c2[k], k, h, ct);
+        }
+    } else {
+        while (cand) {  // two primitives' loads in flight (FLAT: faster despite the registers)
+            const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
+            cand &= cand - 1;
+            const float4_t a0 = m.c0[ka], a1 = m.c1[ka];
+            const c2_t a2 = m.c2[ka];
+            if (cand) {
+                const uint32_t kb = first + uint32_t(__builtin_ctz(cand));
+                cand &= cand - 1;
+                const float4_t b0 = m.c0[kb], b1 = m.c1[kb];
+                const c2_t b2 = m.c2[kb];
+                cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
+                cluster_tri_test<COUNT>(r, b0, b1, b2, kb, h, ct);
+            } else {
+                cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
+            }
         }
     }
 }

@@ -115,21 +115,20 @@ __device__ __forceinline__ void tree_closest_lane(const Ray& r, const DModel& m,
         float bd = -__builtin_inff();
         int32_t bi = -1;
         bool more = true;
-        // The sorted leaves of a pass wait in LDS (a lane-private column, 64 B per lane, 16 KB
-        // per 4-wave workgroup) while they are scanned: the 16 registers of the leaf buffer are
-        // live only during the pass and the scan's registers only during the scan, so the
-        // kernel's peak is the larger of the two, not their sum (no scratch spills at 5
-        // waves/SIMD).
+        // The leaf order buffer lives in LDS (a lane-private column, 64 B per lane, 16 KB per
+        // 4-wave workgroup, trace.h LdsLeafBuf): the pass inserts into it and the scan reads it,
+        // so neither carries its 16 registers (94 VGPRs, no scratch at 5 waves/SIMD; the
+        // register buffer copied to LDS after the pass measured 3% slower).
         __shared__ float s_lbd[4][K][64];
         __shared__ int32_t s_lbl[4][K][64];
         const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
         while (more) {
             int32_t n;
             {
-                LeafBuf<K> lb;
+                LdsLeafBuf<K> lb;
+                lb.d = &s_lbd[w][0][ln];
+                lb.leaf = &s_lbl[w][0][ln];
                 n = traverse_pass<K, COUNT>(r, tab, lb, bd, bi, ct);
-#pragma unroll
-                for (int j = 0; j < K; ++j) { s_lbd[w][j][ln] = lb.d[j]; s_lbl[w][j][ln] = lb.leaf[j]; }
             }
             if (n < 0) { err = 1; break; }
             const int32_t nb = n < K ? n : K;
@@ -289,7 +288,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     for (;;) {
         if (need) {  // one DFS pass (kd_tree.cpp:363-435); its sorted leaves wait in LDS
             int32_t n;
-            {
+            {  // register buffer here: the LDS one (LdsLeafBuf) measured 5% slower in FLAT at C4
                 LeafBuf<K> lb;
                 n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
 #pragma unroll
@@ -357,7 +356,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 lh.slot = 0xFFFFFFFFu;
                 lh.u = lh.v = 0.f;
                 const float4_t lo = m.clus[kClusterBlock * size_t(c)], hi = m.clus[kClusterBlock * size_t(c) + 1];
-                cluster_step<COUNT>(q, m, c, lo, hi, lh, ct);
+                cluster_step<COUNT, true>(q, m, c, lo, hi, lh, ct);
                 if (lh.improved) {
                     mine = (static_cast<unsigned long long>(__float_as_uint(lh.t)) << 32) | uint32_t(lh.rank);
                     atomicMin(&s_key[w][own], mine);

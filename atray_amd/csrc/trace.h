@@ -188,6 +188,40 @@ __device__ __forceinline__ void lb_pop(LeafBuf<K>& b) {
     b.d[K - 1] = __builtin_inff();
 }
 
+// The same buffer held in LDS (lane-private column: entry j of lane ln at word 64 j + ln, no
+// bank conflicts): registers keep only the entry count and the admission bound, so the DFS pass
+// no longer carries 2K registers. An insert shifts the entries with a larger distance up one
+// slot (the last drops out when full): the same order as lb_insert.
+template <int K>
+struct LdsLeafBuf {
+    float* d;       // column base of the distances
+    int32_t* leaf;  // column base of the leaf ids
+    int32_t n;      // entries held
+    float thr;      // d[K - 1] when full, else +inf: an insert needs dis < thr
+};
+
+template <int K>
+__device__ __forceinline__ void lb_clear(LdsLeafBuf<K>& b) {
+    b.n = 0;
+    b.thr = __builtin_inff();
+}
+
+template <int K>
+__device__ __forceinline__ void lb_insert(LdsLeafBuf<K>& b, float dis, int32_t leaf) {
+    if (!(dis < b.thr)) return;
+    int j = b.n < K ? b.n : K - 1;
+    for (; j > 0; --j) {
+        const float pd = b.d[64 * (j - 1)];
+        if (!(pd > dis)) break;
+        b.d[64 * j] = pd;
+        b.leaf[64 * j] = b.leaf[64 * (j - 1)];
+    }
+    b.d[64 * j] = dis;
+    b.leaf[64 * j] = leaf;
+    if (b.n < K) ++b.n;
+    if (b.n == K) b.thr = b.d[64 * (K - 1)];
+}
+
 template <int K>
 __device__ __forceinline__ int32_t lb_leaf(const LeafBuf<K>& b, int j) {
     int32_t r = b.leaf[0];
@@ -223,8 +257,8 @@ __device__ __forceinline__ Inner load_inner(const float4_t* __restrict__ tab, in
 // same f32 operations on the same operands as the reference's per-child slab test
 // (aabb.h:29-93), hence the same bits, computed once per node instead of per child and with
 // no child box loads. Child k: x half = k >> 2, y half = (k >> 1) & 1, z half = k & 1.
-template <int K, bool COUNT>
-__device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, LeafBuf<K>& lb,
+template <int K, bool COUNT, class LB>
+__device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, LB& lb,
                                                   int32_t& ncand, float bd, int32_t bi, Ctr& ct,
                                                   bool first_pass) {
     const float X0 = (n.lx - r.o.x) * r.inv.x, X1 = (n.vx - r.o.x) * r.inv.x, X2 = (n.hx - r.o.x) * r.inv.x;
@@ -277,9 +311,9 @@ __device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, 
 // Per level the stack keeps only the 8-bit mask of inner children still to visit (popped
 // highest first = the reference's LIFO order); a descent reads the child's 48-B record, an
 // ascent the last 16 B of the parent's.
-template <int K, bool COUNT>
+template <int K, bool COUNT, class LB>
 __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* __restrict__ tab,
-                                                 LeafBuf<K>& lb, float bd, int32_t bi, Ctr& ct) {
+                                                 LB& lb, float bd, int32_t bi, Ctr& ct) {
     const bool first_pass = bi < 0;
     if constexpr (COUNT) ct.pass += 1;
     lb_clear<K>(lb);
