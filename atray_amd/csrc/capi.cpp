@@ -163,6 +163,13 @@ int32_t frame_rotate() {
     static const int32_t v = std::max(0, std::min(1024, env_int("ATR_FRAME_ROTATE", 0)));
     return v;
 }
+// HYBRID: a step's leaves are dealt over the lanes in rounds when the largest cluster count
+// exceeds a x rounds + b (render.hip tree_closest_flat); ATR_HYB_A / ATR_HYB_B override.
+void set_hybrid(RenderParams& P) {
+    static const int32_t a = env_int("ATR_HYB_A", 2), b = env_int("ATR_HYB_B", 2);
+    P.hyb_a = a;
+    P.hyb_b = b;
+}
 // PERSIST: 8x8 cells per work-queue chunk (ATR_QCHUNK overrides).
 int32_t qchunk() {
     static const int32_t v = std::max(1, env_int("ATR_QCHUNK", 16));
@@ -418,17 +425,23 @@ int sched_of(int32_t variant) {
         case ATR_KERNEL_CLUSTER: return 4;
         case ATR_KERNEL_PERSIST: return kSchedPersist;
         case ATR_KERNEL_FLAT: return 6;
+        case ATR_KERNEL_HYBRID: return 7;
         case ATR_KERNEL_AUTO: return 4;  // see auto_sched
         default: return variant >= 16 ? variant : 0;
     }
 }
 
 // AUTO: the fastest exact schedule for the camera (measured): primary-only renders
-// (bounce_limit 1, no AA) on lane-private 8x8 cells (CLUSTER, coherent rays), everything else on
-// the flattened cluster rounds (FLAT: incoherent secondary rays diverge at every loop level).
-int auto_sched(int32_t variant, const atr_camera& cam) {
+// (bounce_limit 1, no AA) on lane-private 8x8 cells (CLUSTER, coherent rays) when several frames
+// share the launch (their cells fill the chip while one frame's slowest cells finish), on HYBRID
+// when one frame is alone in its launch (its time is its slowest cells', which HYBRID shortens);
+// everything else on the flattened cluster rounds (FLAT: incoherent secondary rays diverge at
+// every loop level).
+int auto_sched(int32_t variant, const atr_camera& cam, int32_t nframes = 1) {
     if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
-    return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_CLUSTER) : sched_of(ATR_KERNEL_FLAT);
+    if (cam.bounce_limit == 1 && !cam.anti_aliasing)
+        return sched_of(nframes > 1 ? ATR_KERNEL_CLUSTER : ATR_KERNEL_HYBRID);
+    return sched_of(ATR_KERNEL_FLAT);
 }
 
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
@@ -1175,6 +1188,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.error_flag = c->d_error;
     P.counters = nullptr;
     P.xcd_chunk = xcd_chunk();
+    set_hybrid(P);
     const int wave = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(launch_render(c, P, wave, s));
@@ -1232,7 +1246,8 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     P.xcd_chunk = xcd_chunk();
-    const int sched = auto_sched(variant, *cam);
+    set_hybrid(P);
+    const int sched = auto_sched(variant, *cam, nframes);
     HIPCHK(hipEventRecord(c->ev_start, s));
     if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
         P.nblocks = nb * nframes;
@@ -1306,6 +1321,7 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.error_flag = c->d_error;
     P.wave_trace = static_cast<unsigned long long*>(tr.p);
     P.xcd_chunk = xcd_chunk();
+    set_hybrid(P);
     const int ts = sched_of(variant);  // per-cell trace: 8x8-cell schedules only
     HIPCHK(atr_launch_render(P, ts == kSchedPersist ? 4 : ts, nullptr));
     HIPCHK(hipDeviceSynchronize());
@@ -1371,6 +1387,7 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost.p);
     P.xcd_chunk = xcd_chunk();
+    set_hybrid(P);
     HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_CLUSTER), nullptr));  // per-cell clocks
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
@@ -1431,6 +1448,7 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     P.xcd_chunk = xcd_chunk();
+    set_hybrid(P);
     const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     for (int32_t g = 0; g < ngroups; ++g) {

@@ -186,6 +186,7 @@ struct RenderParams {
     int32_t frame_blocks;  // > 0: nblocks = frames x frame_blocks, one launch renders every frame
     int64_t frame_stride;  // output elements between consecutive frames (rgb: 3 x this)
     int32_t frame_rotate;  // frame f's blocks start f / frames x frame_rotate / 1024 into its list
+    int32_t hyb_a, hyb_b;  // HYBRID: a step's leaves are dealt in rounds when max clusters > a x rounds + b
     int32_t nfcam;         // > 0: frame f renders with fcam[f] instead of cam (same size/spp/bounces)
     atr_camera fcam[kMaxFrameCams];
 };

@@ -251,9 +251,17 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
 // CLUSTER's, bit for bit.
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src); }
 
-template <bool COUNT>
+// HYB (the HYBRID schedule): each step the wavefront decides, uniformly, how to scan its rays'
+// current leaves: lane-private (every lane scans its own leaf's clusters, as CLUSTER does: no
+// per-round overhead, best when the rays' cluster counts are alike) or dealt in rounds (FLAT:
+// best when one ray's leaf holds many more clusters than the rest, e.g. the few grazing rays
+// left in a slow cell). It deals when the largest count exceeds a x rounds + b (RenderParams
+// hyb_a / hyb_b). A leaf's result does not depend on how its clusters were visited (minimum
+// (t, leaf rank)), so the choice changes no output bit. LDSB: the DFS pass inserts straight
+// into the LDS columns (CLUSTER's LdsLeafBuf) instead of a register buffer copied after it.
+template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
-                                                  Ctr& ct) {
+                                                  Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
     constexpr unsigned long long kInit = (static_cast<unsigned long long>(0x7F7FFFFFu) << 32) | 0xFFFFFFFFull;
     __shared__ float s_lbd[4][K][64];
@@ -288,7 +296,12 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     for (;;) {
         if (need) {  // one DFS pass (kd_tree.cpp:363-435); its sorted leaves wait in LDS
             int32_t n;
-            {  // register buffer here: the LDS one (LdsLeafBuf) measured 5% slower in FLAT at C4
+            if constexpr (LDSB) {
+                LdsLeafBuf<K> lb;
+                lb.d = &s_lbd[w][0][ln];
+                lb.leaf = &s_lbl[w][0][ln];
+                n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+            } else {  // register buffer here: the LDS one (LdsLeafBuf) measured 5% slower in FLAT at C4
                 LeafBuf<K> lb;
                 n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
 #pragma unroll
@@ -319,8 +332,28 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         const uint32_t excl = incl - cn;
         const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
         s_key[w][ln] = kInit;
+        bool deal = true;
+        if constexpr (HYB) {
+            uint32_t mx = cn;  // the largest cluster count of the step (wave-uniform after the xor tree)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
+            deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
+        }
+        bool lp_imp = false;  // lane-private scan: this lane's leaf improved its hit
+        if (!deal) {
+            if (cn > 0) {
+                LeafHit lh;
+                lh.t = kMaxFloat;
+                lh.slot = 0xFFFFFFFFu;
+                lh.u = lh.v = 0.f;
+                lh.rank = -1;
+                lh.improved = false;
+                cluster_range<COUNT>(r, m, cf, cf + cn, lh, ct);
+                if (lh.improved) { lp_imp = true; res_t = lh.t; res_slot = lh.slot; res_u = lh.u; res_v = lh.v; }
+            }
+        }
         int32_t carry = -1;
-        for (uint32_t base = 0; base < total; base += 64) {  // rounds of 64 items, wave-uniform
+        for (uint32_t base = 0; deal && base < total; base += 64) {  // rounds of 64 items, wave-uniform
             s_mark[w][ln] = -1;
             __builtin_amdgcn_wave_barrier();
             if (cn > 0 && excl >= base && excl < base + 64u) s_mark[w][excl - base] = ln;
@@ -356,7 +389,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 lh.slot = 0xFFFFFFFFu;
                 lh.u = lh.v = 0.f;
                 const float4_t lo = m.clus[kClusterBlock * size_t(c)], hi = m.clus[kClusterBlock * size_t(c) + 1];
-                cluster_step<COUNT, true>(q, m, c, lo, hi, lh, ct);
+                cluster_step<COUNT, PAIR>(q, m, c, lo, hi, lh, ct);
                 if (lh.improved) {
                     mine = (static_cast<unsigned long long>(__float_as_uint(lh.t)) << 32) | uint32_t(lh.rank);
                     atomicMin(&s_key[w][own], mine);
@@ -371,12 +404,18 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             __builtin_amdgcn_wave_barrier();
         }
         if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
-            const unsigned long long key = s_key[w][ln];
-            if (key != kInit) {
-                res_t = __uint_as_float(uint32_t(key >> 32));
-                res_slot = s_slot[w][ln];
-                res_u = s_u[w][ln];
-                res_v = s_v[w][ln];
+            bool imp = lp_imp;
+            if (deal) {
+                const unsigned long long key = s_key[w][ln];
+                imp = key != kInit;
+                if (imp) {
+                    res_t = __uint_as_float(uint32_t(key >> 32));
+                    res_slot = s_slot[w][ln];
+                    res_u = s_u[w][ln];
+                    res_v = s_v[w][ln];
+                }
+            }
+            if (imp) {
                 done = true;
             } else {
                 bd = s_lbd[w][j][ln];
@@ -544,15 +583,16 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 
 // ------------------------------------------------------------------ get_intersection_data
 enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5,
-       SCHED_FLAT = 6 };
+       SCHED_FLAT = 6, SCHED_HYBRID = 7 };
 constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
 constexpr bool sched_coop(int sc) {  // lanes must stay in lockstep loops (workgroup-wide)
-    return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && sc != SCHED_FLAT;
+    return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && sc != SCHED_FLAT &&
+           sc != SCHED_HYBRID;
 }
 
-template <int SCHED, bool COUNT>
+template <int SCHED, bool COUNT, bool PR = false>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
-                                                Isect& id, int& err, Ctr& ct) {
+                                                Isect& id, int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
     float best = kMaxFloat;
     int32_t nm = -1;
@@ -565,6 +605,10 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             Hit h;
             if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_FLAT) tree_closest_flat<COUNT>(r, m, active, h, err, ct);
+            else if constexpr (SCHED == SCHED_HYBRID)
+                // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
+                // bounces: FLAT's register buffer and paired candidate loads (measured)
+                tree_closest_flat<COUNT, true, PR, !PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
@@ -601,7 +645,7 @@ template <int SCHED, bool COUNT>
 __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d, int32_t bounce_limit,
                                        bool active, uint64_t& st, uint64_t stream, uint32_t& casts,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
-                                       int& err, Ctr& ct) {
+                                       int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
     V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
     int32_t i = 0;
     bool live = active;
@@ -609,12 +653,14 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
     // cooperate on leaf scans inside intersect_scene.
     for (i = 0; ; ++i) {
         const bool go = live && i < bounce_limit;
-        if constexpr (SCHED == SCHED_WAVE || SCHED == SCHED_FLAT) { if (__ballot(go) == 0) break; }
+        if constexpr (SCHED == SCHED_WAVE || SCHED == SCHED_FLAT || SCHED == SCHED_HYBRID) {
+            if (__ballot(go) == 0) break;
+        }
         else if constexpr (sched_coop(SCHED)) { if (!__syncthreads_or(go)) break; }
         else if (!go) break;
         Isect id;
         id.type = T_NONE;
-        intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct);
+        intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct, hyb_a, hyb_b);
         if (!go) continue;
         ++traced;
         if (record && i == 0) { hit_face = id.face; hit_t = id.t; }
@@ -710,7 +756,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     if constexpr (PRIMARY) {
         Isect id;
         id.type = T_NONE;
-        intersect_scene<SCHED, COUNT>(S, eye, dir, active, id, err, ct);
+        intersect_scene<SCHED, COUNT, true>(S, eye, dir, active, id, err, ct, P.hyb_a, P.hyb_b);
         if (active) {
             const DMaterial& mat = S->mats[id.material];
             const V3 ret = mk(mat.ex, mat.ey, mat.ez);  // weight (1,1,1) x emission
@@ -731,7 +777,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
             dir = unit(sub(add(add(fc, scale(cx, xo)), scale(cy, yo)), eye));
         }
         col = add(col, cast_ray<SCHED, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
-                                             s == 0, hit_face, hit_t, err, ct));
+                                             s == 0, hit_face, hit_t, err, ct, P.hyb_a, P.hyb_b));
     }
     if (active) {
         col = divs(col, float(cm.samples_per_pixel));  // :358
@@ -798,7 +844,10 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
 #define ATR_INST(SC, C, PR) template __global__ void render_kernel<SC, C, PR>(RenderParams);
 #define ATR_INST4(SC) ATR_INST(SC, false, false) ATR_INST(SC, true, false) ATR_INST(SC, false, true) ATR_INST(SC, true, true)
 ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCHED_TILE8) ATR_INST4(SCHED_CLUSTER)
-ATR_INST4(SCHED_FLAT)
+ATR_INST4(SCHED_FLAT) ATR_INST4(SCHED_HYBRID)
+template __global__ void render_kernel<SCHED_HYBRID, false, true, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_HYBRID, false, true, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_HYBRID, false, false, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, false, 5>(RenderParams);
@@ -886,6 +935,14 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);
+    if (sched >= 80) {  // HYBRID at 80 + n waves/SIMD (diagnostic)
+        const int o = sched - 80;
+        if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 5>), g, b, 0, s, P);
+        else if (!count && o == 6 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 6>), g, b, 0, s, P);
+        else if (!count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, false, 5>), g, b, 0, s, P);
+        else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
+        return hipGetLastError();
+    }
     if (sched >= 64) {  // FLAT at 64 + n waves/SIMD (diagnostic)
         const int o = sched - 64;
         if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 5>), g, b, 0, s, P);
@@ -924,6 +981,7 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     switch (sched) {
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
         case 6: launch_sched<atr::SCHED_FLAT>(P, count, prim, s); break;
+        case 7: launch_sched<atr::SCHED_HYBRID>(P, count, prim, s); break;  // 4 waves/SIMD (measured)
         case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;
         case 3: launch_sched<atr::SCHED_TILE8>(P, count, prim, s); break;
         case 4:

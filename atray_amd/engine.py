@@ -24,6 +24,7 @@ ATR_KERNEL_WAVEFRONT = 5
 ATR_KERNEL_CLUSTER = 6
 ATR_KERNEL_PERSIST = 7
 ATR_KERNEL_FLAT = 8
+ATR_KERNEL_HYBRID = 9
 MISS = 0xFFFFFFFF
 MAX_FLOAT = np.float32(3.402823466e38)
 

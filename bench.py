@@ -202,13 +202,16 @@ def launch_sizes(k, f):
     return [k // n + (1 if i < k % n else 0) for i in range(n)]
 
 
+VARIANT_NAMES = {}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps", "flat"])
+    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps", "flat", "hyb"])
     ap.add_argument("--variant-code", type=int, default=-1,
                     help="diagnostic: raw kernel code passed to the engine (overrides --variant's kernel)")
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
@@ -345,7 +348,9 @@ def run(args):
     variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE,
                "tile": E.ATR_KERNEL_TILE, "tile8": E.ATR_KERNEL_TILE8,
                "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
-               "ps": E.ATR_KERNEL_PERSIST, "flat": E.ATR_KERNEL_FLAT}[args.variant]
+               "ps": E.ATR_KERNEL_PERSIST, "flat": E.ATR_KERNEL_FLAT, "hyb": E.ATR_KERNEL_HYBRID}[args.variant]
+    VARIANT_NAMES.update({E.ATR_KERNEL_AUTO: "auto", E.ATR_KERNEL_CLUSTER: "cluster", E.ATR_KERNEL_FLAT: "flat",
+                          E.ATR_KERNEL_HYBRID: "hybrid", E.ATR_KERNEL_PERSIST: "persist", E.ATR_KERNEL_LANE: "lane"})
     if args.variant_code >= 0:
         variant = args.variant_code
     # ---- scene prep (untimed for Mrays/s; reported under "prep")
@@ -513,18 +518,29 @@ def run(args):
         check = mism if args.check else None
         casts_frames = sum(nf for _, nf in last.values())
 
-    # ---- single frame (app camera, one frame per launch): the roofline kernel
+    # ---- the roofline kernel: the timed launches' schedule, one app-camera frame per launch,
+    # serialized (AUTO resolves per launch shape: CLUSTER when several frames share a launch,
+    # HYBRID for one frame alone, FLAT for bounces; capi.cpp auto_sched)
+    primary = bounces == 1
+    roof_variant = variant
+    if variant == E.ATR_KERNEL_AUTO:
+        roof_variant = E.ATR_KERNEL_FLAT if not primary else (E.ATR_KERNEL_CLUSTER if F_ > 1 else E.ATR_KERNEL_HYBRID)
     s0 = streams[0]
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-    for a, b in evs:
-        a.record(s0)
-        eng.render_start(app_cam, tiles, frame_of(0), SEED, stream=s0.cuda_stream, variant=variant)
-        b.record(s0)
-    torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    rc, _ = eng.wait()
-    assert rc == 0
-    live_ctr = eng.counters(app_cam, tiles, SEED, variant) if rank == 0 else None
+
+    def time_one(v, n=10):
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for a, b in evs:
+            a.record(s0)
+            eng.render_start(app_cam, tiles, frame_of(0), SEED, stream=s0.cuda_stream, variant=v)
+            b.record(s0)
+        torch.cuda.synchronize()
+        rc, _ = eng.wait()
+        assert rc == 0
+        return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms = time_one(roof_variant)
+    # one frame alone in its launch with the variant as given (AUTO: the latency schedule)
+    alone_ms = kern_ms if roof_variant == variant else time_one(variant)
+    live_ctr = eng.counters(app_cam, tiles, SEED, roof_variant) if rank == 0 else None
 
     if rank == 0:
         value = rays_total / elapsed / 1e6
@@ -546,11 +562,11 @@ def run(args):
         if check is not None:
             out["check_mismatched_pixels"] = check
         n1 = live_ctr["n_rays"]
-        out["single_frame"] = {"kernel_ms": round(kern_ms, 4), "mrays_s": round(n1 / kern_ms / 1e3, 1),
-                               "camera": "app", "rays": n1}
+        out["single_frame"] = {"kernel_ms": round(alone_ms, 4), "mrays_s": round(n1 / alone_ms / 1e3, 1),
+                               "camera": "app", "rays": n1, "variant": VARIANT_NAMES.get(variant, variant)}
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
-        clustered = args.variant in ("auto", "cl", "ps", "flat")
+        clustered = args.variant in ("auto", "cl", "ps", "flat", "hyb")
         bpr = cluster_bytes_per_ray(live_ctr) if clustered else algorithmic_bytes_per_ray(live_ctr)
         achieved = bpr * n1 / (kern_ms * 1e-3) / 1e9
         roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -567,6 +583,7 @@ def run(args):
         # AUTO: CLUSTER cells for primary-only renders, FLAT cells otherwise (both render_kernel)
         kname = "persist_kernel" if args.variant == "ps" else "render_kernel"
         roof["kernel"] = kname
+        roof["variant"] = VARIANT_NAMES.get(roof_variant, roof_variant)
         if world == 1 and not args.no_pmc:
             traffic, why = pmc_traffic(args, kname)
             roof["traffic"] = traffic

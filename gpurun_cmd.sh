@@ -1,12 +1,14 @@
 export TMPDIR=/tmp
-O=gpurun_out/r02
+O=gpurun_out/r02c
 mkdir -p $O
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c3 -o run -- python3 bench.py --no-cpu-baseline --no-pmc > $O/bench_c3_traced.json 2> $O/trace_c3.err || exit 1
-python tools/trace_summary.py $O/trace_c3 4 > $O/trace_c3_summary.json || exit 1
-OUT_DIR=r02/pmc bash tools/gpu_pmc2.sh > $O/pmc.log 2>&1 || exit 1
-python tools/pmc_summary2.py $O/pmc > $O/pmc_summary.json || exit 1
-timeout -k 10 300 python bench.py --config c4 --steps 4 --warmup 1 > $O/bench_c4.json || exit 1
-timeout -k 10 400 python bench.py --config c5 --steps 2 --warmup 1 > $O/bench_c5.json || exit 1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c4 -o run -- python3 bench.py --config c4 --steps 4 --warmup 1 --no-cpu-baseline --no-pmc --no-prep > $O/bench_c4_traced.json 2> $O/trace_c4.err || exit 1
-python tools/trace_summary.py $O/trace_c4 4 > $O/trace_c4_summary.json || exit 1
+for ab in "2 2" "2 1" "2 0" "3 1" "2 3" "3 2" "1 1"; do set -- $ab
+  ATR_HYB_A=$1 ATR_HYB_B=$2 timeout -k 10 120 python tools/kprof.py --variants cl,hyb --rounds 7 > $O/kp_c3_$1_$2.json || exit 1
+done
+for ab in "2 2" "4 4" "8 8" "1 0"; do set -- $ab
+  ATR_HYB_A=$1 ATR_HYB_B=$2 timeout -k 10 200 python tools/kprof.py --config c4 --variants flat,hyb --rounds 2 --iters 1 > $O/kp_c4_$1_$2.json || exit 1
+done
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc --variant cl > $O/bench_c3_cl.json || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc --variant hyb > $O/bench_c3_hyb.json || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc --variant cl > $O/bench_c3_cl2.json || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc --variant hyb > $O/bench_c3_hyb2.json || exit 1
 echo done

@@ -185,7 +185,9 @@ enum { ATR_KERNEL_AUTO = 0, ATR_KERNEL_LANE = 1, ATR_KERNEL_WAVE = 2, ATR_KERNEL
        ATR_KERNEL_TILE8 = 4, ATR_KERNEL_WAVEFRONT = 5, ATR_KERNEL_CLUSTER = 6,
        ATR_KERNEL_PERSIST = 7 /* persistent waves, lanes refilled from per-XCD work queues */,
        ATR_KERNEL_FLAT = 8 /* clustered scan, the wavefront's (ray, cluster) work dealt over its
-                              lanes in rounds (no control-flow divergence in the scan) */ };
+                              lanes in rounds (no control-flow divergence in the scan) */,
+       ATR_KERNEL_HYBRID = 9 /* per leaf step: lane-private scans when the rays' cluster counts
+                                are alike, FLAT rounds when one ray's leaf dominates */ };
 
 /* start_render_from_camera: renders the pixels of `tiles` (inclusive rects; overlapping pixels
    are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the null stream, HIP's convention). RNG: deterministic per-pixel PCG stream from `seed` (DESIGN.md "RNG"). Returns

@@ -71,7 +71,7 @@ def test_cluster_scan_bit_exact_on_grazing_soup(eng, seed, n, det, leaf):
     eng.upload([SKY, MODEL], [(m, tree, m.aabb(), 1)], (), ())
     hit = face_o != 0xFFFFFFFF
     assert hit.sum() > 1000, hit.sum()   # the soup must actually be hit
-    for variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT):
+    for variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID):
         o = run(eng, cam, variant=variant)
         bad = np.argwhere((o["face"] != face_o) | (o["t"].view(np.uint32) != t_o.view(np.uint32)))
         assert len(bad) == 0, (variant, len(bad), bad[:5].tolist())

@@ -97,7 +97,8 @@ C4_BANDS = [(552, 560), (312, 316)]
 C5_BANDS = [(1112, 1114), (626, 627)]
 
 
-@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST])
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
+                                     E.ATR_KERNEL_HYBRID])
 def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
     """C4 through AUTO (= FLAT for multi-bounce, capi.cpp auto_sched), CLUSTER and FLAT."""
     o = render(eng, E.camera(1920, 1080, 64, 5), variant)
@@ -112,7 +113,7 @@ def test_c4_schedules_agree_at_full_size(eng):
     frames, and a re-render is identical (determinism)."""
     cam = E.camera(1920, 1080, 64, 5)
     a = render(eng, cam, E.ATR_KERNEL_PERSIST)
-    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT):
+    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID):
         b = render(eng, cam, v)
         for k in ("fb", "casts", "face"):
             assert torch.equal(a[k], b[k]), (v, k)
@@ -133,7 +134,7 @@ ORBIT = [(0.1 + 0.5 * np.sin(a), 2.0, 0.5 * (1 - np.cos(a))) for a in np.linspac
 
 
 @pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
-                                     E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT])
+                                     E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID])
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (2, 3)])
 @pytest.mark.parametrize("layout", [E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED])
 def test_per_frame_cameras_equal_single_renders(eng, variant, spp, bounces, layout):

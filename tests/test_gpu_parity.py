@@ -19,7 +19,7 @@ SKY, MODEL = O.SKY, O.MODEL_MAT
 # The parity triad: CLUSTER (primary-only default), PERSIST (multi-bounce default) and LANE (the
 # reference's exact per-triangle work). The slower experimental schedules (WAVE, TILE4/8,
 # WAVEFRONT) run only with ATR_TEST_ALL_VARIANTS=1.
-VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT]
+VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID]
 if os.environ.get("ATR_TEST_ALL_VARIANTS") == "1":
     VARIANTS += [E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8, E.ATR_KERNEL_WAVEFRONT]
 RGB_RTOL = 1e-5
@@ -342,7 +342,7 @@ def test_gpu_work_counters_equal_reference_work(eng, name, variant):
     c = eng.counters(E.camera(g["W"], g["H"]), [[0, 0, g["W"] - 1, g["H"] - 1]], SEED, variant)
     for k in ["n_rays", "n_box", "n_leaf"]:
         assert c[k] == g["counters"][k], (k, c[k], g["counters"][k])
-    if variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT) and g["tree"]:
+    if variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID) and g["tree"]:
         # the clustered scan visits the same leaves but skips provably irrelevant triangles
         assert 0 < c["n_tri"] <= g["counters"]["n_tri"], (c["n_tri"], g["counters"]["n_tri"])
     else:

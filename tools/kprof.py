@@ -47,10 +47,16 @@ def main():
              "tile8": E.ATR_KERNEL_TILE8, "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
              "ps": E.ATR_KERNEL_PERSIST, "occ4": 20, "occ5": 21,
              "occ6": 22, "occ8": 24, "cl4": 36, "cl5": 37, "cl6": 38, "cl8": 40,
-             "k4o4": 52, "k4o5": 53, "k4o6": 54, "k4o8": 56}
+             "k4o4": 52, "k4o5": 53, "k4o6": 54, "k4o8": 56, "flat": E.ATR_KERNEL_FLAT,
+             "hyb": E.ATR_KERNEL_HYBRID, "fl4": 68, "fl5": 69, "hyb4": 84, "hyb5": 85, "hyb6": 86}
     vs = args.variants.split(",")
     res = {v: [] for v in vs}
-    ctrs = {v: eng.counters(cam, tiles, SEED, names[v] if names[v] in (1, 2, 3, 4, 6, 7) else (E.ATR_KERNEL_CLUSTER if names[v] >= 32 else E.ATR_KERNEL_LANE)) for v in vs}
+    def ctr_variant(code):
+        if code < 16: return code
+        if code >= 80: return E.ATR_KERNEL_HYBRID
+        if code >= 64: return E.ATR_KERNEL_FLAT
+        return E.ATR_KERNEL_CLUSTER if code >= 32 else E.ATR_KERNEL_LANE
+    ctrs = {v: eng.counters(cam, tiles, SEED, ctr_variant(names[v])) for v in vs}
     for v in vs:  # warm
         eng.render_start(cam, tiles, fr, SEED, stream=stream, variant=names[v])
     torch.cuda.synchronize()
@@ -63,7 +69,8 @@ def main():
             b.record()
             torch.cuda.synchronize()
             res[v].append(a.elapsed_time(b) / args.iters)
-    out = {"config": args.config, "W": W, "H": H, "spp": spp, "bounces": bounces}
+    out = {"config": args.config, "W": W, "H": H, "spp": spp, "bounces": bounces,
+           "hyb": [os.environ.get("ATR_HYB_A"), os.environ.get("ATR_HYB_B")]}
     for v in vs:
         c = ctrs[v]
         ms = float(np.median(res[v]))
