@@ -467,6 +467,11 @@ def run(args):
         for j in sorted(pending):
             assemble(j)
 
+    # setup, not warmup: one small launch on every stream (a stream's first launch pays its
+    # hardware-queue setup, ~ms) so the timed region does not depend on W reaching every stream
+    for q in range(S_):
+        eng.render_start_cameras([cams[0]], tiles, frame_of(q), npf, SEED, stream=streams[q].cuda_stream,
+                                 variant=variant)
     torch.cuda.synchronize()
     run_frames(0, args.warmup)
     torch.cuda.synchronize()
