@@ -432,16 +432,12 @@ int sched_of(int32_t variant) {
 }
 
 // AUTO: the fastest exact schedule for the camera (measured): primary-only renders
-// (bounce_limit 1, no AA) on lane-private 8x8 cells (CLUSTER, coherent rays) when several frames
-// share the launch (their cells fill the chip while one frame's slowest cells finish), on HYBRID
-// when one frame is alone in its launch (its time is its slowest cells', which HYBRID shortens);
-// everything else on the flattened cluster rounds (FLAT: incoherent secondary rays diverge at
-// every loop level).
-int auto_sched(int32_t variant, const atr_camera& cam, int32_t nframes = 1) {
+// (bounce_limit 1, no AA) on HYBRID cells (lane-private leaf scans for coherent rays, dealt rounds
+// for the stragglers), everything else on the flattened cluster rounds (FLAT: incoherent
+// secondary rays diverge at every loop level).
+int auto_sched(int32_t variant, const atr_camera& cam) {
     if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
-    if (cam.bounce_limit == 1 && !cam.anti_aliasing)
-        return sched_of(nframes > 1 ? ATR_KERNEL_CLUSTER : ATR_KERNEL_HYBRID);
-    return sched_of(ATR_KERNEL_FLAT);
+    return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_HYBRID) : sched_of(ATR_KERNEL_FLAT);
 }
 
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
@@ -1247,7 +1243,7 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
     P.error_flag = c->d_error;
     P.xcd_chunk = xcd_chunk();
     set_hybrid(P);
-    const int sched = auto_sched(variant, *cam, nframes);
+    const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
         P.nblocks = nb * nframes;

@@ -259,7 +259,7 @@ __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src
 // hyb_a / hyb_b). A leaf's result does not depend on how its clusters were visited (minimum
 // (t, leaf rank)), so the choice changes no output bit. LDSB: the DFS pass inserts straight
 // into the LDS columns (CLUSTER's LdsLeafBuf) instead of a register buffer copied after it.
-template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true>
+template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
@@ -348,7 +348,8 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 lh.u = lh.v = 0.f;
                 lh.rank = -1;
                 lh.improved = false;
-                cluster_range<COUNT>(r, m, cf, cf + cn, lh, ct);
+                for (uint32_t c = cf; c < cf + cn; ++c)
+                    cluster_step<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1], lh, ct);
                 if (lh.improved) { lp_imp = true; res_t = lh.t; res_slot = lh.slot; res_u = lh.u; res_v = lh.v; }
             }
         }
@@ -370,7 +371,8 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             const bool valid = k < total;
             const int32_t src = valid ? own : ln;
             Ray q;  // the owner's ray
-            q.o = mk(shfl_f(r.o.x, src), shfl_f(r.o.y, src), shfl_f(r.o.z, src));
+            // UO: every ray of the wave starts at the same point (primary rays: the frame's eye)
+            q.o = UO ? r.o : mk(shfl_f(r.o.x, src), shfl_f(r.o.y, src), shfl_f(r.o.z, src));
             q.d = mk(shfl_f(r.d.x, src), shfl_f(r.d.y, src), shfl_f(r.d.z, src));
             q.inv = mk(shfl_f(r.inv.x, src), shfl_f(r.inv.y, src), shfl_f(r.inv.z, src));
             q.s0 = q.inv.x < 0;
@@ -608,7 +610,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (SCHED == SCHED_HYBRID)
                 // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
                 // bounces: FLAT's register buffer and paired candidate loads (measured)
-                tree_closest_flat<COUNT, true, PR, !PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                tree_closest_flat<COUNT, true, PR, !PR, PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
@@ -641,11 +643,21 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
 }
 
 // ------------------------------------------------------------------ cast_ray + pixel loop
+// Path state parked in LDS while a ray is traced (the FLAT/HYBRID bounce kernels): the colour
+// sums, throughput, PCG state and counters are dead during the tree query, so a lane-private LDS
+// column holds them instead of registers the query needs (16 KB per 4-wave workgroup).
+constexpr int kStash = 16;
+__device__ __forceinline__ void stash_put(uint32_t* L, int k, float v) { L[64 * k] = __float_as_uint(v); }
+__device__ __forceinline__ float stash_getf(const uint32_t* L, int k) { return __uint_as_float(L[64 * k]); }
+
 template <int SCHED, bool COUNT>
 __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d, int32_t bounce_limit,
                                        bool active, uint64_t& st, uint64_t stream, uint32_t& casts,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
-                                       int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
+                                       int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b, V3& acc) {
+    constexpr bool STASH = SCHED == SCHED_FLAT || SCHED == SCHED_HYBRID;
+    __shared__ uint32_t s_stash[STASH ? 4 : 1][kStash][64];
+    uint32_t* L = &s_stash[STASH ? threadIdx.x >> 6 : 0][0][threadIdx.x & 63];
     V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
     int32_t i = 0;
     bool live = active;
@@ -660,7 +672,23 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
         else if (!go) break;
         Isect id;
         id.type = T_NONE;
+        if constexpr (STASH) {
+            stash_put(L, 0, ret.x); stash_put(L, 1, ret.y); stash_put(L, 2, ret.z);
+            stash_put(L, 3, w.x); stash_put(L, 4, w.y); stash_put(L, 5, w.z);
+            stash_put(L, 6, acc.x); stash_put(L, 7, acc.y); stash_put(L, 8, acc.z);
+            L[64 * 9] = uint32_t(st); L[64 * 10] = uint32_t(st >> 32);
+            L[64 * 11] = casts; L[64 * 12] = traced; L[64 * 13] = hit_face; stash_put(L, 14, hit_t);
+            __asm__ volatile("" ::: "memory");  // the values below come back from LDS
+        }
         intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct, hyb_a, hyb_b);
+        if constexpr (STASH) {
+            __asm__ volatile("" ::: "memory");
+            ret = mk(stash_getf(L, 0), stash_getf(L, 1), stash_getf(L, 2));
+            w = mk(stash_getf(L, 3), stash_getf(L, 4), stash_getf(L, 5));
+            acc = mk(stash_getf(L, 6), stash_getf(L, 7), stash_getf(L, 8));
+            st = uint64_t(L[64 * 9]) | (uint64_t(L[64 * 10]) << 32);
+            casts = L[64 * 11]; traced = L[64 * 12]; hit_face = L[64 * 13]; hit_t = stash_getf(L, 14);
+        }
         if (!go) continue;
         ++traced;
         if (record && i == 0) { hit_face = id.face; hit_t = id.t; }
@@ -777,7 +805,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
             dir = unit(sub(add(add(fc, scale(cx, xo)), scale(cy, yo)), eye));
         }
         col = add(col, cast_ray<SCHED, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
-                                             s == 0, hit_face, hit_t, err, ct, P.hyb_a, P.hyb_b));
+                                             s == 0, hit_face, hit_t, err, ct, P.hyb_a, P.hyb_b, col));
     }
     if (active) {
         col = divs(col, float(cm.samples_per_pixel));  // :358
@@ -981,7 +1009,10 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     switch (sched) {
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
         case 6: launch_sched<atr::SCHED_FLAT>(P, count, prim, s); break;
-        case 7: launch_sched<atr::SCHED_HYBRID>(P, count, prim, s); break;  // 4 waves/SIMD (measured)
+        case 7:  // primaries at 5 waves/SIMD (measured: DESIGN.md §4e)
+            if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 5>), g, b, 0, s, P);
+            else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
+            break;
         case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;
         case 3: launch_sched<atr::SCHED_TILE8>(P, count, prim, s); break;
         case 4:

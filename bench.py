@@ -524,12 +524,10 @@ def run(args):
         casts_frames = sum(nf for _, nf in last.values())
 
     # ---- the roofline kernel: the timed launches' schedule, one app-camera frame per launch,
-    # serialized (AUTO resolves per launch shape: CLUSTER when several frames share a launch,
-    # HYBRID for one frame alone, FLAT for bounces; capi.cpp auto_sched)
-    primary = bounces == 1
+    # serialized (AUTO: HYBRID for primary-only frames, FLAT for bounces; capi.cpp auto_sched)
     roof_variant = variant
     if variant == E.ATR_KERNEL_AUTO:
-        roof_variant = E.ATR_KERNEL_FLAT if not primary else (E.ATR_KERNEL_CLUSTER if F_ > 1 else E.ATR_KERNEL_HYBRID)
+        roof_variant = E.ATR_KERNEL_HYBRID if bounces == 1 else E.ATR_KERNEL_FLAT
     s0 = streams[0]
 
     def time_one(v, n=10):
@@ -543,8 +541,6 @@ def run(args):
         assert rc == 0
         return float(np.mean([a.elapsed_time(b) for a, b in evs]))
     kern_ms = time_one(roof_variant)
-    # one frame alone in its launch with the variant as given (AUTO: the latency schedule)
-    alone_ms = kern_ms if roof_variant == variant else time_one(variant)
     live_ctr = eng.counters(app_cam, tiles, SEED, roof_variant) if rank == 0 else None
 
     if rank == 0:
@@ -567,8 +563,8 @@ def run(args):
         if check is not None:
             out["check_mismatched_pixels"] = check
         n1 = live_ctr["n_rays"]
-        out["single_frame"] = {"kernel_ms": round(alone_ms, 4), "mrays_s": round(n1 / alone_ms / 1e3, 1),
-                               "camera": "app", "rays": n1, "variant": VARIANT_NAMES.get(variant, variant)}
+        out["single_frame"] = {"kernel_ms": round(kern_ms, 4), "mrays_s": round(n1 / kern_ms / 1e3, 1),
+                               "camera": "app", "rays": n1, "variant": VARIANT_NAMES.get(roof_variant, roof_variant)}
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel_ms": round(kern_ms, 4)}
         clustered = args.variant in ("auto", "cl", "ps", "flat", "hyb")
