@@ -166,7 +166,7 @@ int32_t frame_rotate() {
 // HYBRID: a step's leaves are dealt over the lanes in rounds when the largest cluster count
 // exceeds a x rounds + b (render.hip tree_closest_flat); ATR_HYB_A / ATR_HYB_B override.
 void set_hybrid(RenderParams& P) {
-    static const int32_t a = env_int("ATR_HYB_A", 2), b = env_int("ATR_HYB_B", 2);
+    static const int32_t a = env_int("ATR_HYB_A", 2), b = env_int("ATR_HYB_B", 1);
     P.hyb_a = a;
     P.hyb_b = b;
 }

@@ -259,7 +259,7 @@ __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src
 // hyb_a / hyb_b). A leaf's result does not depend on how its clusters were visited (minimum
 // (t, leaf rank)), so the choice changes no output bit. LDSB: the DFS pass inserts straight
 // into the LDS columns (CLUSTER's LdsLeafBuf) instead of a register buffer copied after it.
-template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false>
+template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false, bool UT = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
@@ -294,7 +294,20 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     uint32_t res_slot = 0xFFFFFFFFu;
     float res_t = kMaxFloat, res_u = 0.f, res_v = 0.f;
     for (;;) {
-        if (need) {  // one DFS pass (kd_tree.cpp:363-435); its sorted leaves wait in LDS
+        if constexpr (UT) {  // the wave walks its passes together (traverse_pass_wave)
+            if (__ballot(need)) {
+                LdsLeafBuf<K> lb;
+                lb.d = &s_lbd[w][0][ln];
+                lb.leaf = &s_lbl[w][0][ln];
+                const int32_t n = traverse_pass_wave<K, COUNT>(r, m.inner, lb, bd, bi, ct, need);
+                if (need) {
+                    need = false;
+                    j = 0;
+                    if (n < 0) { err = 1; done = true; }
+                    else { nb = n < K ? n : K; more = n > K; if (nb == 0) done = true; }
+                }
+            }
+        } else if (need) {  // one DFS pass (kd_tree.cpp:363-435); its sorted leaves wait in LDS
             int32_t n;
             if constexpr (LDSB) {
                 LdsLeafBuf<K> lb;
@@ -610,7 +623,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (SCHED == SCHED_HYBRID)
                 // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
                 // bounces: FLAT's register buffer and paired candidate loads (measured)
-                tree_closest_flat<COUNT, true, PR, !PR, PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                tree_closest_flat<COUNT, true, PR, !PR, PR, PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {

@@ -250,6 +250,32 @@ __device__ __forceinline__ Inner load_inner(const float4_t* __restrict__ tab, in
     return n;
 }
 
+// The same record at a wave-uniform index, read by the scalar unit into SGPRs (one fetch per
+// wavefront, no VGPRs for the record): s_load of 32 + 16 bytes. The table is read-only for the
+// kernel's lifetime, so the scalar cache cannot hold a stale copy.
+typedef uint32_t u32x8_t __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Inner load_inner_uniform(const float4_t* __restrict__ tab, int32_t i) {
+    const uint64_t a64 = reinterpret_cast<uint64_t>(tab + 3 * i);
+    const uint64_t u64 = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int32_t(uint32_t(a64))))) |
+                         (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int32_t(uint32_t(a64 >> 32))))) << 32);
+    const float4_t* p = reinterpret_cast<const float4_t*>(u64);
+    u32x8_t a;
+    u32x4_t c;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(a), "=s"(c)
+                 : "s"(p));
+    Inner n;
+    n.lx = __uint_as_float(a[0]); n.ly = __uint_as_float(a[1]); n.lz = __uint_as_float(a[2]);
+    n.vx = __uint_as_float(a[3]); n.vy = __uint_as_float(a[4]); n.vz = __uint_as_float(a[5]);
+    n.hx = __uint_as_float(a[6]); n.hy = __uint_as_float(a[7]);
+    n.hz = __uint_as_float(c[0]);
+    n.leaf0 = int32_t(c[1]);
+    n.parent = int32_t(c[2]);
+    n.bm = c[3];
+    return n;
+}
+
 // Examine the children of an inner node (kd_tree.cpp:370-434): box-test children in order
 // until 5 have been hit; inner hits -> returned bit mask, leaf hits -> leaf order buffer.
 // The children boxes are the octants of (lo, v, hi) (kd_tree.cpp:116-148), so every slab
@@ -348,6 +374,55 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
         }
     }
     return ncand;
+}
+
+// The same pass walked by the whole wavefront (coherent primary rays): the wave visits the union
+// of its lanes' DFS paths in the common order (highest inner child first, each subtree before
+// the next), reading each inner record once per wave with scalar loads; a lane examines a node
+// only if its own pass would visit it (the node is in the lane's own child mask), so every lane
+// discovers exactly the leaves -- with the same distances and static ranks -- its lane-private
+// pass discovers, in the same order. Called by every lane of the wave (converged); `part` = this
+// lane runs a pass. Returns the lane's candidate count (-1: tree deeper than the mask stack).
+template <int K, bool COUNT, class LB>
+__device__ __forceinline__ int32_t traverse_pass_wave(const Ray& r, const float4_t* __restrict__ tab, LB& lb,
+                                                      float bd, int32_t bi, Ctr& ct, bool part) {
+    const bool first_pass = bi < 0;
+    if constexpr (COUNT) { if (part) ct.pass += 1; }
+    if (part) lb_clear<K>(lb);
+    int32_t ncand = 0;
+    Inner cur = load_inner_uniform(tab, 0);
+    uint64_t lo = part ? uint64_t(examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass)) : 0;
+    uint64_t hi = 0;
+    uint32_t bm = cur.bm;  // wave-uniform walk state
+    int32_t parent = -1, lvl = 0;
+    for (;;) {
+        const uint32_t mine = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
+        int s = -1;  // highest child any lane still has to visit at this level
+        for (int b = 7; b >= 0; --b)
+            if (__ballot((mine >> b) & 1u)) { s = b; break; }
+        if (s >= 0) {
+            const bool act = (mine >> s) & 1u;
+            if (lvl < 8) lo &= ~(uint64_t(1) << (8 * lvl + s));
+            else hi &= ~(uint64_t(1) << (8 * (lvl - 8) + s));
+            const uint32_t innerm = ~bm & ((1u << s) - 1u);
+            const int32_t id = int32_t(bm >> 8) + __popc(innerm);
+            cur = load_inner_uniform(tab, id);
+            const uint64_t cm = act ? uint64_t(examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass)) : 0;
+            ++lvl;
+            if (lvl >= kMaskLevels) return -1;
+            if (lvl < 8) lo |= cm << (8 * lvl);
+            else hi |= cm << (8 * (lvl - 8));
+            bm = cur.bm;
+            parent = cur.parent;
+        } else {
+            if (lvl == 0) break;
+            --lvl;
+            const Inner p = load_inner_uniform(tab, parent);
+            bm = p.bm;
+            parent = p.parent;
+        }
+    }
+    return part ? ncand : 0;
 }
 
 }  // namespace atr

@@ -1,11 +1,15 @@
 export TMPDIR=/tmp
-O=gpurun_out/r02g
+O=gpurun_out/r02j
 mkdir -p $O
 PT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 600 $PT tests/test_gpu_parity.py tests/test_gpu_cluster.py -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 600 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
-timeout -k 10 120 python tools/kprof.py --variants cl,hyb4,hyb5 --rounds 7 > $O/kp_c3.json || exit 1
-for v in 84 85 36 37; do
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc --variant-code $v > $O/bench_c3_$v.json || exit 1
+timeout -k 10 120 python tools/kprof.py --variants cl5,hyb4,hyb5 --rounds 7 > $O/kp_c3.json || exit 1
+python -c "
+import json; d=json.load(open('$O/kp_c3.json')); print({k:(v['ms_median'],v['ms_min']) for k,v in d.items() if isinstance(v,dict)})"
+for i in 1 2; do
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-pmc > $O/bench_c3_$i.json || exit 1
+python -c "
+import json; d=json.load(open('$O/bench_c3_$i.json')); print('c3', d['value'], d['ms_per_step'], d['single_frame']['kernel_ms'])"
 done
 echo done
