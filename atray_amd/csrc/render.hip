@@ -251,6 +251,21 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
 // CLUSTER's, bit for bit.
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src); }
 
+// LDS of the FLAT/HYBRID scans (22.5 KB per 4-wave workgroup): the leaf order buffers (lane-private
+// columns), the per-owner best keys and hit records, the round's owner markers.
+struct FlatLds {
+    float lbd[4][kLeafBuf][64];
+    int32_t lbl[4][kLeafBuf][64];
+    unsigned long long key[4][64];
+    uint32_t slot[4][64];
+    float u[4][64], v[4][64];
+    int32_t mark[4][64];
+};
+__device__ __forceinline__ FlatLds& flat_lds() {
+    __shared__ FlatLds L;
+    return L;
+}
+
 // HYB (the HYBRID schedule): each step the wavefront decides, uniformly, how to scan its rays'
 // current leaves: lane-private (every lane scans its own leaf's clusters, as CLUSTER does: no
 // per-round overhead, best when the rays' cluster counts are alike) or dealt in rounds (FLAT:
@@ -264,12 +279,14 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
     constexpr unsigned long long kInit = (static_cast<unsigned long long>(0x7F7FFFFFu) << 32) | 0xFFFFFFFFull;
-    __shared__ float s_lbd[4][K][64];
-    __shared__ int32_t s_lbl[4][K][64];
-    __shared__ unsigned long long s_key[4][64];
-    __shared__ uint32_t s_slot[4][64];
-    __shared__ float s_u[4][64], s_v[4][64];
-    __shared__ int32_t s_mark[4][64];
+    FlatLds& L = flat_lds();  // one instance per kernel, shared by every flavour of this scan
+    auto& s_lbd = L.lbd;
+    auto& s_lbl = L.lbl;
+    auto& s_key = L.key;
+    auto& s_slot = L.slot;
+    auto& s_u = L.u;
+    auto& s_v = L.v;
+    auto& s_mark = L.mark;
     const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
     h.t = kMaxFloat;
     h.face = 0;
@@ -607,7 +624,8 @@ constexpr bool sched_coop(int sc) {  // lanes must stay in lockstep loops (workg
 
 template <int SCHED, bool COUNT, bool PR = false>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
-                                                Isect& id, int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
+                                                Isect& id, int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b,
+                                                bool first = false) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
     float best = kMaxFloat;
     int32_t nm = -1;
@@ -619,7 +637,11 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
             Hit h;
             if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
-            else if constexpr (SCHED == SCHED_FLAT) tree_closest_flat<COUNT>(r, m, active, h, err, ct);
+            else if constexpr (SCHED == SCHED_FLAT) {
+                // the camera rays of a bounce loop (one origin, coherent) take HYBRID's primary flavour
+                if (first) tree_closest_flat<COUNT, true, true, false, true, true>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                else tree_closest_flat<COUNT>(r, m, active, h, err, ct);
+            }
             else if constexpr (SCHED == SCHED_HYBRID)
                 // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
                 // bounces: FLAT's register buffer and paired candidate loads (measured)
@@ -693,7 +715,7 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
             L[64 * 11] = casts; L[64 * 12] = traced; L[64 * 13] = hit_face; stash_put(L, 14, hit_t);
             __asm__ volatile("" ::: "memory");  // the values below come back from LDS
         }
-        intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct, hyb_a, hyb_b);
+        intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct, hyb_a, hyb_b, i == 0);
         if constexpr (STASH) {
             __asm__ volatile("" ::: "memory");
             ret = mk(stash_getf(L, 0), stash_getf(L, 1), stash_getf(L, 2));
