@@ -631,7 +631,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
     int32_t nm = -1;
     uint32_t face = 0;
     float fu = 0.f, fv = 0.f;
-    const int32_t nmodels = S->nmodels;
+    const int32_t nmodels = __builtin_amdgcn_readfirstlane(S->nmodels);  // uniform: an SGPR, not a VGPR
     for (int32_t i = 0; i < nmodels; ++i) {
         const DModel& m = S->models[i];
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
@@ -842,7 +842,19 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         col = add(col, cast_ray<SCHED, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
                                              s == 0, hit_face, hit_t, err, ct, P.hyb_a, P.hyb_b, col));
     }
-    if (active) {
+    // the output address from the cell record read again (PRIMARY): the pixel coordinates and mask
+    // then hold no registers through the trace (the asm clobber keeps the compiler from reusing
+    // the first read)
+    DBlock ob = blk;
+    if constexpr (PRIMARY) {
+        __asm__ volatile("" ::: "memory");
+        if (in_range) ob = P.blocks[bi];
+    }
+    int olane = int(threadIdx.x);
+    if constexpr (PRIMARY) __asm__ volatile("" : "+v"(olane));  // recomputed here, not kept from the start
+    olane &= 63;
+    const uint64_t omask = uint64_t(ob.mask_lo) | (uint64_t(ob.mask_hi) << 32);
+    if ((omask >> olane) & 1) {
         col = divs(col, float(cm.samples_per_pixel));  // :358
         const float cr = pl_max(0.0f, pl_min(col.x, 1.0f));
         const float cg = pl_max(0.0f, pl_min(col.y, 1.0f));
@@ -850,8 +862,8 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         const uint32_t r8 = uint32_t(cr * 255.0f) & 0xFFu, g8 = uint32_t(cg * 255.0f) & 0xFFu,
                        b8 = uint32_t(cb * 255.0f) & 0xFFu;
         size_t o;
-        if (P.layout == ATR_LAYOUT_PACKED) o = size_t(blk.out_base) + __popcll(mask & ((uint64_t(1) << lane) - 1));
-        else o = size_t(y) * size_t(cm.width) + size_t(x);
+        if (P.layout == ATR_LAYOUT_PACKED) o = size_t(ob.out_base) + __popcll(omask & ((uint64_t(1) << olane) - 1));
+        else o = size_t(ob.y0 + (olane >> 3)) * size_t(cm.width) + size_t(ob.x0 + (olane & 7));
         o += size_t(fidx) * size_t(P.frame_stride);
         P.framebuffer[o] = b8 | (g8 << 8) | (r8 << 16);  // Set_Pixel (texture.h:27-38)
         if (P.hit_face) P.hit_face[o] = hit_face;

@@ -19,7 +19,8 @@ struct Isect {
 __device__ __forceinline__ void scene_finish(const DScene* __restrict__ S, V3 o, V3 d, float best, uint32_t face,
                                              float fu, float fv, int32_t nm, Isect& id) {
     int32_t ns = -1, np = -1;
-    for (int32_t i = 0; i < S->nspheres; ++i) {  // sphere.h:12-39
+    const int32_t nspheres = __builtin_amdgcn_readfirstlane(S->nspheres), nplanes = __builtin_amdgcn_readfirstlane(S->nplanes);
+    for (int32_t i = 0; i < nspheres; ++i) {  // sphere.h:12-39
         const DSphere& sp = S->spheres[i];
         const V3 pc = sub(o, mk(sp.cx, sp.cy, sp.cz));
         const float pcs = len2(pc);
@@ -37,7 +38,7 @@ __device__ __forceinline__ void scene_finish(const DScene* __restrict__ S, V3 o,
         }
         if (t > kTol && t < best) { best = t; ns = i; }
     }
-    for (int32_t i = 0; i < S->nplanes; ++i) {  // plane.h:12-22
+    for (int32_t i = 0; i < nplanes; ++i) {  // plane.h:12-22
         const DPlane& pl = S->planes[i];
         const V3 n = mk(pl.nx, pl.ny, pl.nz);
         const float denom = dot(n, d);

@@ -1,16 +1,13 @@
 export TMPDIR=/tmp
-O=gpurun_out/r02m
+O=gpurun_out/r02n
 mkdir -p $O
 PT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 timeout -k 10 600 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
-timeout -k 10 120 python tools/kprof.py --variants cl5,hyb5 --rounds 5 > $O/kp_c3.json || exit 1
+timeout -k 10 120 python tools/kprof.py --variants cl5,hyb5 --rounds 7 > $O/kp_c3.json || exit 1
 python -c "
 import json; d=json.load(open('$O/kp_c3.json')); print({k:(v['ms_median'],v['ms_min']) for k,v in d.items() if isinstance(v,dict)})"
-timeout -k 10 200 python tools/kprof.py --config c4 --variants flat --rounds 2 --iters 1 > $O/kp_c4.json || exit 1
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_c3.json || exit 1
 python -c "
-import json; d=json.load(open('$O/kp_c4.json')); print({k:(v['ms_median'],v['ms_min']) for k,v in d.items() if isinstance(v,dict)})"
-timeout -k 10 300 python bench.py --config c4 --steps 16 --warmup 1 --no-cpu-baseline --no-pmc --no-prep > $O/bench_c4.json || exit 1
-python -c "
-import json; d=json.load(open('$O/bench_c4.json')); print('c4', d['value'], d['ms_per_step'])"
+import json; d=json.load(open('$O/bench_c3.json')); print('c3', d['value'], d['ms_per_step'], d['single_frame']['kernel_ms'], d['roofline']['traffic'])"
 echo done

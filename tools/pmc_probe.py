@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import atray_amd.engine as E  # noqa: E402
 from atray_amd.assets import CENTERS, asset_path  # noqa: E402
 
-variant = int(os.environ.get("PMC_VARIANT", str(E.ATR_KERNEL_CLUSTER)))
+variant = int(os.environ.get("PMC_VARIANT", str(E.ATR_KERNEL_AUTO)))
 W, H = 1920, 1080
 mesh = E.Mesh.load_obj(asset_path("Dragon"))
 box = mesh.translate_to(mesh.aabb(), CENTERS["Dragon"])
