@@ -777,7 +777,8 @@ __device__ __forceinline__ int remap_xcd(int wg, int nwg, int chunk) {
 template <int SCHED, bool COUNT, bool PRIMARY, int OCC = 4>
 __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(RenderParams P) {
     constexpr int NW = sched_waves(SCHED);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index is uniform: in an SGPR, so are the cell and frame indices derived from it
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const int b = remap_xcd(blockIdx.x, gridDim.x, P.xcd_chunk) * NW + wave;
     if (SCHED != SCHED_TILE4 && SCHED != SCHED_TILE8 && b >= P.nblocks) return;  // whole wavefront
     const bool in_range = b < P.nblocks;
@@ -842,16 +843,14 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         col = add(col, cast_ray<SCHED, COUNT>(S, eye, dir, cm.bounce_limit, active, st, stream, casts, traced,
                                              s == 0, hit_face, hit_t, err, ct, P.hyb_a, P.hyb_b, col));
     }
-    // the output address from the cell record read again (PRIMARY): the pixel coordinates and mask
+    // the output address from the cell record read again: the pixel coordinates and mask
     // then hold no registers through the trace (the asm clobber keeps the compiler from reusing
     // the first read)
     DBlock ob = blk;
-    if constexpr (PRIMARY) {
-        __asm__ volatile("" ::: "memory");
-        if (in_range) ob = P.blocks[bi];
-    }
+    __asm__ volatile("" ::: "memory");
+    if (in_range) ob = P.blocks[bi];
     int olane = int(threadIdx.x);
-    if constexpr (PRIMARY) __asm__ volatile("" : "+v"(olane));  // recomputed here, not kept from the start
+    __asm__ volatile("" : "+v"(olane));  // recomputed here, not kept from the start
     olane &= 63;
     const uint64_t omask = uint64_t(ob.mask_lo) | (uint64_t(ob.mask_hi) << 32);
     if ((omask >> olane) & 1) {
