@@ -194,11 +194,14 @@ def spawn_ranks(n):
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
-def launch_sizes(k, f):
-    """k frames in launches of at most f, sizes as equal as possible."""
+def launch_sizes(k, f, s=1):
+    """k frames in launches of at most f, sizes as equal as possible, the launch count a multiple
+    of the s streams they are dealt to round-robin (so every stream ends with the same work and
+    none runs its last launch alone: 20 frames at f=4, s=2 -> 4,4,3,3,3,3, not 4,4,4,4,4)."""
     if k <= 0:
         return []
     n = (k + f - 1) // f
+    n = min(k, (n + s - 1) // s * s)
     return [k // n + (1 if i < k % n else 0) for i in range(n)]
 
 
@@ -457,7 +460,7 @@ def run(args):
 
     def run_frames(k0, k, on_launch=None):
         j0 = 0
-        for nf in launch_sizes(k, F_):
+        for nf in launch_sizes(k, F_, S_):
             q = j0 % S_
             launch(j0, k0, nf, q)
             if on_launch:
@@ -502,7 +505,7 @@ def run(args):
     if rank == 0:
         ref = torch.zeros(W * H, dtype=torch.int32, device=dev)
         refc = torch.zeros(W * H, dtype=torch.int32, device=dev)
-        sizes_l = launch_sizes(args.steps, F_)
+        sizes_l = launch_sizes(args.steps, F_, S_)
         k0 = args.warmup
         last = {}
         for j, nf in enumerate(sizes_l):
@@ -557,7 +560,7 @@ def run(args):
                           "parallelism": f"tiles{world}", "kernel": args.variant,
                           "plan": args.plan if world > 1 else "single",
                           "streams": args.streams, "frames_per_launch": F_,
-                          "launches": launch_sizes(args.steps, F_),
+                          "launches": launch_sizes(args.steps, F_, S_),
                           "shard_pixels": [int(x) for x in sizes]},
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
         if check is not None:

@@ -44,11 +44,17 @@ def test_bench_rejects_world_size_mismatch():
 
 
 @pytest.mark.parametrize("k,f", [(20, 8), (48, 8), (7, 8), (1, 1), (17, 16), (0, 8)])
-def test_launch_sizes_are_balanced(k, f):
-    s = bench.launch_sizes(k, f)
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_launch_sizes_are_balanced(k, f, streams):
+    s = bench.launch_sizes(k, f, streams)
     assert sum(s) == k and all(1 <= x <= f for x in s)
     assert (max(s) - min(s) <= 1) if s else k == 0
-    assert len(s) == (k + f - 1) // f
+    n = (k + f - 1) // f
+    # fewest launches that is a multiple of the streams (or one launch per frame)
+    assert len(s) == min(k, -(-n // streams) * streams)
+    if k >= streams:  # round-robin: every stream gets the same frames, to one
+        per = [sum(s[q::streams]) for q in range(streams)]
+        assert max(per) - min(per) <= 1
 
 
 def test_orbit_cameras_are_distinct():
