@@ -226,7 +226,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="launches in flight (one HIP stream each)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch; "
-                         "0 = 4 x ranks (each rank's launch keeps about 4 full frames of work)")
+                         "0 = the K steps in as few launches per stream as the cap allows, at least 4 x ranks "
+                         "(a launch boundary inside a stream and the last launch's tail are the overheads)")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
@@ -243,7 +244,7 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.frames_per_launch <= 0:
-        args.frames_per_launch = 4 * world
+        args.frames_per_launch = max(4 * world, -(-args.steps // max(1, args.streams)))
     args.frames_per_launch = max(1, min(16, args.frames_per_launch))
     if args.selftest:
         return selftest(args)
