@@ -32,6 +32,9 @@ extern "C" hipError_t atr_wf_render(const atr::WFParams& W, int32_t nmodels, con
                                     const int32_t* has_tree, int32_t* pinned, hipStream_t s);
 extern "C" hipError_t atr_launch_tile_casts(const atr_tile* tiles, int32_t ntiles, int32_t width,
                                             const uint32_t* casts, int64_t* out, hipStream_t s);
+extern "C" hipError_t atr_launch_packed_tile_casts(const int32_t* slot_tile, int64_t nslots, const uint32_t* casts,
+                                                   int64_t frame_stride, int32_t nframes, int32_t ntiles,
+                                                   unsigned long long* out, hipStream_t s);
 
 #define HIPCHK(x)                                      \
     do {                                               \
@@ -55,6 +58,8 @@ struct BlockSet {
     DevBuf dev;
     DevBuf dev_tiles;
     DevBuf dev_pix;  // pixel index per packed slot (wavefront schedule)
+    DevBuf dev_tile;  // owning tile per packed slot (atr_packed_tile_ray_casts; built on first use)
+    bool tile_ready = false;
     int64_t packed_pixels = 0;
     hipEvent_t ev = nullptr;  // recorded on the stream of every launch that reads this set
     bool used = false;
@@ -372,6 +377,7 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
         b.used = false;
     }
     b.tiles.assign(tiles, tiles + ntiles);
+    b.tile_ready = false;
     b.width = W;
     b.height = H;
     build_blocks(tiles, ntiles, W, H, b.host, b.packed_pixels);
@@ -758,6 +764,7 @@ int atr_destroy(atr_ctx* c) {
         if (b.dev.p) (void)hipFree(b.dev.p);
         if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
         if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
+        if (b.dev_tile.p) (void)hipFree(b.dev_tile.p);
         if (b.ev) (void)hipEventDestroy(b.ev);
     }
     for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
@@ -1548,6 +1555,57 @@ int atr_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_
     HIPCHK(atr_launch_tile_casts(static_cast<const atr_tile*>(dt), ntiles, width, casts, out, s));
     HIPCHK(hipFreeAsync(dt, s));
     HIPCHK(hipStreamSynchronize(s));
+    return ATR_OK;
+}
+
+int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width, int32_t height,
+                              const uint32_t* casts, int32_t nframes, int64_t frame_stride, int64_t* out,
+                              void* stream) {
+    if (!c || !casts || !out || width <= 0 || height <= 0 || ntiles < 0 || (ntiles && !tiles) || nframes < 0 ||
+        nframes > 65535)
+        return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, width, height, rc);  // the render's cached set
+    if (!bs) return rc;
+    if (nframes > 1 && frame_stride < bs->packed_pixels) return ATR_E_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
+    const int64_t n = bs->packed_pixels;
+    if (!bs->tile_ready) {  // owner of every pixel = the first tile holding it (packed: traced once)
+        std::vector<int32_t> owner(size_t(width) * size_t(height), -1);
+        for (int32_t k = 0; k < ntiles; ++k) {
+            const int32_t x0 = std::max(tiles[k].min_x, 0), x1 = std::min(tiles[k].max_x, width - 1);
+            const int32_t y0 = std::max(tiles[k].min_y, 0), y1 = std::min(tiles[k].max_y, height - 1);
+            for (int32_t y = y0; y <= y1; ++y)
+                for (int32_t x = x0; x <= x1; ++x) {
+                    int32_t& o = owner[size_t(y) * size_t(width) + size_t(x)];
+                    if (o < 0) o = k;
+                }
+        }
+        std::vector<int32_t> st(size_t(n > 0 ? n : 1), -1);
+        size_t k = 0;
+        for (const DBlock& blk : bs->host) {
+            const uint64_t m = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+            for (int lane = 0; lane < 64; ++lane)
+                if ((m >> lane) & 1)
+                    st[k++] = owner[size_t(blk.y0 + (lane >> 3)) * size_t(width) + size_t(blk.x0 + (lane & 7))];
+        }
+        // a hipMemcpy below may overwrite a buffer a kernel on another stream still reads
+        if (bs->used) HIPCHK(hipEventSynchronize(bs->ev));
+        const size_t need = st.size() * sizeof(int32_t);
+        if (bs->dev_tile.n < need) {
+            if (bs->dev_tile.p) (void)hipFree(bs->dev_tile.p);
+            bs->dev_tile = DevBuf();
+            if (hipMalloc(&bs->dev_tile.p, need) != hipSuccess) return ATR_E_NOMEM;
+            bs->dev_tile.n = need;
+        }
+        HIPCHK(hipMemcpy(bs->dev_tile.p, st.data(), need, hipMemcpyHostToDevice));
+        bs->tile_ready = true;
+    }
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(int64_t) * size_t(nframes) * size_t(ntiles), s));
+    HIPCHK(atr_launch_packed_tile_casts(static_cast<const int32_t*>(bs->dev_tile.p), n, casts, frame_stride, nframes,
+                                        ntiles, reinterpret_cast<unsigned long long*>(out), s));
+    HIPCHK(note_launch(c, s, bs));
     return ATR_OK;
 }
 

@@ -983,6 +983,32 @@ __global__ __launch_bounds__(256) void tile_casts_kernel(const atr_tile* __restr
     if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 
+// Per-tile sums of a PACKED ray_casts buffer, frame blockIdx.y: slot i adds to the tile that owns
+// its pixel (slot_tile, host-built per tile list). A shard tile's slots are one contiguous run, so
+// a wave's 64 slots almost always share the tile: one wave reduction + one atomic per wave.
+__global__ __launch_bounds__(256) void packed_tile_casts_kernel(const int32_t* __restrict__ slot_tile,
+                                                                int64_t nslots,
+                                                                const uint32_t* __restrict__ casts,
+                                                                int64_t frame_stride, int32_t ntiles,
+                                                                unsigned long long* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t f = blockIdx.y;
+    int32_t t = -1;
+    unsigned long long v = 0;
+    if (i < nslots) {
+        t = slot_tile[i];
+        v = casts[f * frame_stride + i];
+    }
+    const int32_t t0 = __builtin_amdgcn_readfirstlane(t);
+    if (__ballot(t != t0) == 0) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0 && t0 >= 0 && v) atomicAdd(&out[f * ntiles + t0], v);
+    } else if (t >= 0 && v) {
+        atomicAdd(&out[f * ntiles + t], v);
+    }
+}
+
 }  // namespace atr
 
 // launchers used by capi.cpp
@@ -1080,6 +1106,16 @@ extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nbloc
     const int grid = (nblocks + 3) / 4;
     if (grid <= 0) return hipSuccess;
     hipLaunchKernelGGL(atr::unpack_kernel, dim3(grid), dim3(256), 0, s, blocks, nblocks, width, packed, image);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t atr_launch_packed_tile_casts(const int32_t* slot_tile, int64_t nslots, const uint32_t* casts,
+                                                   int64_t frame_stride, int32_t nframes, int32_t ntiles,
+                                                   unsigned long long* out, hipStream_t s) {
+    const int64_t grid = (nslots + 255) / 256;
+    if (grid <= 0 || nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(atr::packed_tile_casts_kernel, dim3(unsigned(grid), unsigned(nframes)), dim3(256), 0, s,
+                       slot_tile, nslots, casts, frame_stride, ntiles, out);
     return hipGetLastError();
 }
 

@@ -96,7 +96,7 @@ EXPORTS = [
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
-    "atr_mesh_export",
+    "atr_mesh_export", "atr_packed_tile_ray_casts",
 ]
 
 _lib = None
@@ -148,6 +148,7 @@ def lib():
         "atr_packed_pixel_map": ([vp, i32, i32, i32, vp, i64], i64),
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
+        "atr_packed_tile_ray_casts": ([vp, vp, i32, i32, i32, vp, i32, i64, vp, vp], C.c_int),
         "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
         "atr_render_start_progressive": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32, i32],
                                          C.c_int),
@@ -489,6 +490,14 @@ class Engine:
         check(lib().atr_tile_ray_casts(self.h, C.cast(arr, C.c_void_p), n, int(width),
                                        C.c_void_p(casts_ptr), C.c_void_p(out_ptr),
                                        C.c_void_p(stream) if stream else None), "tile casts")
+
+    def packed_tile_ray_casts(self, tiles, width, height, casts_ptr, nframes, frame_stride, out_ptr, stream=None):
+        """out[f * ntiles + i] (device int64) = ray_casts of tile i in PACKED frame f (asynchronous)."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_packed_tile_ray_casts(self.h, C.cast(arr, C.c_void_p), n, int(width), int(height),
+                                              C.c_void_p(casts_ptr), int(nframes), int(frame_stride),
+                                              C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None),
+              "packed tile casts")
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

@@ -1,12 +1,13 @@
 """Image sharding across ranks (one process per GPU) and the frame gather to rank 0.
 
 Pixels are independent given the replicated read-only scene, so the frame is
-split into square shard tiles dealt round-robin to ranks (interleaved: per-tile cost varies
-~3.4x across the reference demo's tiles, centre >> edge). Each rank traces its tiles into a
-packed buffer (every owned pixel once, tile order); the one exchange step is a gather of the
-packed buffers to rank 0 (RCCL over xGMI for backend "nccl"; gloo in the CPU tests), where
-they are scattered into the image. Each pixel's spp/bounce loop stays on one rank, so the
-result is bit-identical to a single-GPU render.
+split into square shard tiles dealt to ranks (longest-first by measured cost, or round-robin:
+per-tile cost varies ~3.4x across the reference demo's tiles, centre >> edge). Each rank traces
+its tiles into a packed buffer (every owned pixel once, tile order); the one exchange step is
+an exact-size gather of the packed framebuffers to rank 0 (`gather_frames`: RCCL send/recv over
+xGMI for backend "nccl"; gloo in the CPU tests), where they are scattered into the image, plus
+a reduction of the per-tile ray_casts sums (a few KB). Each pixel's spp/bounce loop stays on
+one rank, so the result is bit-identical to a single-GPU render.
 """
 from __future__ import annotations
 
@@ -20,26 +21,34 @@ class ShardPlan:
     (atr_make_shard_tiles). With `owner` (one rank per grid tile, e.g. from `balanced`): that
     assignment, each rank's tiles kept in grid order."""
 
-    def __init__(self, width: int, height: int, world: int, side: int = 64, owner=None):
+    def __init__(self, width: int, height: int, world: int, side: int = 64, owner=None, costs=None):
         self.width, self.height, self.world, self.side = width, height, world, side
-        if owner is None:
+        if owner is None and costs is None:
             self.tiles = [E.make_shard_tiles(width, height, side, r, world) for r in range(world)]
         else:
             grid = E.shard_grid(width, height, side)
+            if owner is None:
+                owner = np.arange(len(grid)) % world
             owner = np.asarray(owner, np.int32)
             assert len(owner) == len(grid) and owner.min() >= 0 and owner.max() < world
-            self.tiles = [grid[owner == r] for r in range(world)]
+            idx = np.arange(len(grid))
+            if costs is not None:  # each rank's tiles heaviest first: a launch starts its slowest cells
+                idx = np.argsort(-np.asarray(costs, np.int64), kind="stable")  # first, so they do not form its tail
+            self.tiles = [grid[idx[owner[idx] == r]] for r in range(world)]
         self.owner = owner
         self.sizes = [E.packed_size(t) if len(t) else 0 for t in self.tiles]
         self.max_size = max(1, max(self.sizes))
 
     @classmethod
-    def balanced(cls, costs, width: int, height: int, world: int, side: int = 64, rank0_extra: float = 0.0):
+    def balanced(cls, costs, width: int, height: int, world: int, side: int = 64, rank0_extra: float = 0.0,
+                 heavy_first: bool = True):
         """Longest-first deal by measured per-tile cost (`tile_costs`); rank 0 starts with
-        rank0_extra x the mean per-rank load (its frame assembly)."""
+        rank0_extra x the mean per-rank load (its frame assembly). heavy_first: each rank's tiles
+        in descending cost (else grid order)."""
         costs = np.asarray(costs, np.int64)
         extra = int(rank0_extra * costs.sum() / max(1, world))
-        return cls(width, height, world, side, E.balance_shard_tiles(width, height, side, world, costs, extra))
+        owner = E.balance_shard_tiles(width, height, side, world, costs, extra)
+        return cls(width, height, world, side, owner, costs if heavy_first else None)
 
     def pixel_map(self, rank: int) -> np.ndarray:
         return E.packed_pixel_map(self.tiles[rank], self.width, self.height)
@@ -78,6 +87,76 @@ def gather_packed(packed, plan: ShardPlan, rank: int, dist, group=None):
     lst = [torch.empty_like(packed) for _ in range(plan.world)] if rank == 0 else None
     dist.gather(packed, lst, dst=0, group=group)
     return lst
+
+
+def frame_offsets(plan: ShardPlan, nframes: int) -> list:
+    """Start of rank r's block in the exact gather buffer: every rank's F packed frames back to
+    back, rank after rank (F x size_r elements each, no padding)."""
+    off = np.concatenate([[0], np.cumsum(np.asarray(plan.sizes, np.int64) * nframes)])
+    return [int(x) for x in off]
+
+
+def frames_assembly_index(plan: ShardPlan, nframes: int) -> np.ndarray:
+    """Destination of every element of the exact gather buffer (frame_offsets) in nframes images
+    of width x height: element i of rank r's frame f goes to f * W * H + pixel_map(r)[i]. The
+    shard tiles partition the image, so the buffer is exactly nframes * W * H long and one
+    index_copy_ assembles a whole launch."""
+    npx = plan.width * plan.height
+    parts = []
+    for r in range(plan.world):
+        if plan.sizes[r] == 0:
+            continue
+        m = plan.pixel_map(r).astype(np.int64)
+        parts.append((np.arange(nframes, dtype=np.int64)[:, None] * npx + m[None, :]).ravel())
+    out = np.concatenate(parts)
+    assert out.size == nframes * npx
+    return out
+
+
+def slot_tiles(plan: ShardPlan, rank: int) -> np.ndarray:
+    """Shard-grid tile (row-major index in shard_grid order) of every packed slot of `rank`: the
+    per-tile ray_casts sums (the reference's per-tile counters, renderer.cpp:465-468) are
+    index_add_ reductions over it."""
+    if plan.sizes[rank] == 0:
+        return np.zeros(0, np.int64)
+    m = plan.pixel_map(rank).astype(np.int64)
+    ntx = -(-plan.width // plan.side)
+    return (m // plan.width // plan.side) * ntx + (m % plan.width) // plan.side
+
+
+def tile_ids(plan: ShardPlan, rank: int) -> np.ndarray:
+    """Shard-grid index of each of `rank`'s tiles, in its tile-list order."""
+    t = np.asarray(plan.tiles[rank]).reshape(-1, 4).astype(np.int64)
+    ntx = -(-plan.width // plan.side)
+    return (t[:, 1] // plan.side) * ntx + t[:, 0] // plan.side
+
+
+def pixel_tiles(width: int, height: int, side: int) -> np.ndarray:
+    """Shard-grid tile of every pixel of an IMAGE-layout frame (y * width + x)."""
+    ntx = -(-width // side)
+    y, x = np.divmod(np.arange(width * height, dtype=np.int64), width)
+    return (y // side) * ntx + x // side
+
+
+def grid_tile_count(plan: ShardPlan) -> int:
+    return (-(-plan.width // plan.side)) * (-(-plan.height // plan.side))
+
+
+def gather_frames(send, recv, plan: ShardPlan, rank: int, nframes: int, dist):
+    """Exact-size gather of nframes packed frames to rank 0 (the one exchange step: RCCL send/recv
+    over xGMI for backend "nccl"). `send`: this rank's frames back to back (nframes x size_r
+    elements; rank 0's own block is written in place by its render). `recv` (rank 0): the exact
+    gather buffer (frame_offsets with the launch's frame capacity F). Returns the async works."""
+    ops = []
+    if rank == 0:
+        off = frame_offsets(plan, recv.numel() // (plan.width * plan.height))
+        for r in range(1, plan.world):
+            n = plan.sizes[r] * nframes
+            if n:
+                ops.append(dist.P2POp(dist.irecv, recv[off[r]:off[r] + n], r))
+    elif plan.sizes[rank]:
+        ops.append(dist.P2POp(dist.isend, send[:plan.sizes[rank] * nframes], 0))
+    return dist.batch_isend_irecv(ops) if ops else []
 
 
 def scatter_host(bufs, plan: ShardPlan) -> np.ndarray:

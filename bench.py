@@ -230,10 +230,20 @@ def main():
                          "(a launch boundary inside a stream and the last launch's tail are the overheads)")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
+    ap.add_argument("--calib-frames", type=int, default=3,
+                    help="cost plan: per-tile costs summed over this many of the run's frames (one calibration render each)")
+    ap.add_argument("--tile-order", default="cost", choices=["cost", "grid"],
+                    help="N>1 (and --single-tiles cost): each rank's tiles heaviest first (default) or in grid order")
+    ap.add_argument("--single-tiles", default="frame", choices=["frame", "cost"],
+                    help="N=1 tile list: one full-frame tile (default) or the shard grid, heaviest tiles first")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
                     help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
     ap.add_argument("--check", action="store_true",
                     help="rank 0: compare every assembled frame with a one-launch full-frame render")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="diagnostic, one process: render only rank --sim-rank's shard of a --sim-world plan "
+                         "(packed outputs, per-tile ray_casts sums; no exchange): the per-rank render side of an N-GPU run")
+    ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--selftest", action="store_true",
                     help="CPU only: synthetic fill instead of the render kernel (launch/plan/gather test)")
     args = ap.parse_args()
@@ -244,30 +254,18 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.frames_per_launch <= 0:
-        args.frames_per_launch = max(4 * world, -(-args.steps // max(1, args.streams)))
+        args.frames_per_launch = max(4 * max(world, args.sim_world), -(-args.steps // max(1, args.streams)))
     args.frames_per_launch = max(1, min(16, args.frames_per_launch))
     if args.selftest:
         return selftest(args)
     return run(args)
 
 
-def frame_assembly(plan, F, world):
-    """Destination of every slot of the gathered buffer [world][2][F][maxn] (framebuffer frames,
-    then ray_casts frames) in a buffer holding F frame images and F ray_casts images, each W*H + 1
-    long (the extra element takes the plan's padding slots)."""
-    import numpy as np
-    from atray_amd import shard as S
-    npx = plan.width * plan.height + 1
-    one = S.assembly_index(plan).reshape(world, 1, 1, plan.max_size)
-    part = np.arange(2, dtype=np.int64).reshape(1, 2, 1, 1) * (F * npx)
-    frame = np.arange(F, dtype=np.int64).reshape(1, 1, F, 1) * npx
-    return np.ascontiguousarray(one + part + frame).ravel()
-
-
 def selftest(args):
-    """Launch + shard plan + gather + assembly on CPU (gloo) with a synthetic fill: rank r writes
-    pixel index + 7 f into its packed framebuffer slots of frame f and (pixel % 5) into ray_casts.
-    Rank 0 checks every assembled frame and the total_ray_casts sum."""
+    """Launch + shard plan + exact gather + assembly + per-tile ray_casts reduction on CPU (gloo)
+    with a synthetic fill in place of the render kernel: rank r writes pixel index + 7 k into its
+    packed framebuffer slots of frame k and (pixel % 5) into ray_casts. Rank 0 checks every
+    assembled frame and every shard tile's ray_casts sum."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -283,34 +281,40 @@ def selftest(args):
     plan = S.ShardPlan.balanced(costs, W, H, world, side, args.rank0_extra) if args.plan == "cost" \
         else S.ShardPlan(W, H, world, side)
     F = args.frames_per_launch
-    pix = plan.pixel_map(rank)
-    maxn = plan.max_size
-    dst = torch.from_numpy(frame_assembly(plan, F, world))
+    pix = torch.from_numpy(plan.pixel_map(rank).astype(np.int64)) if plan.sizes[rank] else torch.zeros(0, dtype=torch.int64)
+    own = plan.sizes[rank]
+    off = S.frame_offsets(plan, F)
+    dst = torch.from_numpy(S.frames_assembly_index(plan, F))
+    stile = torch.from_numpy(S.slot_tiles(plan, rank))
+    ngrid = S.grid_tile_count(plan)
+    want_tiles = torch.zeros(ngrid, dtype=torch.int64).index_add_(
+        0, torch.from_numpy(S.pixel_tiles(W, H, side)), torch.arange(W * H) % 5)
     mism, casts_ok, frames = 0, True, 0
     t0 = time.perf_counter()
-    for j, nf in enumerate(launch_sizes(args.steps, F)):
-        buf = torch.zeros(2 * F * maxn, dtype=torch.int64)
+    k = 0
+    for nf in launch_sizes(args.steps, F):
+        big = torch.zeros(F * W * H, dtype=torch.int64)
+        fb = big[off[0]:off[0] + F * own] if rank == 0 else torch.zeros(F * own, dtype=torch.int64)
+        casts = torch.zeros(F, own, dtype=torch.int64)
         for f in range(nf):
-            k = j * F + f
-            buf[f * maxn:f * maxn + len(pix)] = torch.from_numpy(pix + 7 * k)
-            buf[(F + f) * maxn:(F + f) * maxn + len(pix)] = torch.from_numpy(pix % 5)
-        big = torch.zeros(world * 2 * F * maxn, dtype=torch.int64)
+            fb[f * own:(f + 1) * own] = pix + 7 * (k + f)
+            casts[f] = pix % 5
+        tsum = torch.zeros(F, ngrid, dtype=torch.int64).index_add_(1, stile, casts)
         if world > 1:
-            dist.gather(buf, list(big.chunk(world)) if rank == 0 else None, dst=0)
-        else:
-            big.copy_(buf)
+            works = S.gather_frames(fb, big, plan, rank, nf, dist)
+            works.append(dist.reduce(tsum, dst=0, async_op=True))
+            for w_ in works:
+                w_.wait()
         if rank == 0:
-            npx = W * H + 1
-            img = torch.zeros(2 * F * npx, dtype=torch.int64)
+            img = torch.zeros(F * W * H, dtype=torch.int64)
             img.index_copy_(0, dst, big)
-            want = np.arange(W * H, dtype=np.int64)
+            want = torch.arange(W * H, dtype=torch.int64)
             for f in range(nf):
-                k = j * F + f
-                got = img[f * npx:f * npx + W * H].numpy()
-                mism += int((got != want + 7 * k).sum())
-                casts = img[(F + f) * npx:(F + f) * npx + W * H].numpy()
-                casts_ok &= int(casts.sum()) == int((want % 5).sum())
+                got = img[f * W * H:(f + 1) * W * H]
+                mism += int((got != want + 7 * (k + f)).sum())
+                casts_ok &= bool(torch.equal(tsum[f], want_tiles))
                 frames += 1
+        k += nf
     elapsed = time.perf_counter() - t0
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
@@ -387,56 +391,80 @@ def run(args):
 
     # ---- shard plan (untimed): one calibration render measures every grid tile's cost on rank 0,
     # broadcast so all ranks derive the same longest-first deal
-    if world > 1 and args.plan == "cost":
-        costs = S.tile_costs(eng, app_cam, W, H, args.side, SEED) if rank == 0 else np.zeros(
-            len(E.shard_grid(W, H, args.side)), np.int64)
-        costs = S.shared_costs(costs, rank, dist, dev if backend == "nccl" else "cpu")
-        plan = S.ShardPlan.balanced(costs, W, H, world, args.side, args.rank0_extra)
+    sim = world == 1 and args.sim_world > 1
+    pw, pr = (args.sim_world, args.sim_rank) if sim else (world, rank)  # the plan's world and rank
+    heavy_first = args.tile_order == "cost"
+    if (pw > 1 and args.plan == "cost") or (pw == 1 and args.single_tiles == "cost"):
+        # measured on a few of the run's own frames (a live renderer would use its previous frames)
+        ks = sorted({args.warmup + (args.steps * i) // max(1, args.calib_frames) for i in range(args.calib_frames)})
+        costs = np.zeros(len(E.shard_grid(W, H, args.side)), np.int64)
+        if rank == 0:
+            for k in ks:
+                costs += S.tile_costs(eng, cams[k % n_orbit], W, H, args.side, SEED)
+        if world > 1:
+            costs = S.shared_costs(costs, rank, dist, dev if backend == "nccl" else "cpu")
+        plan = S.ShardPlan.balanced(costs, W, H, pw, args.side, args.rank0_extra, heavy_first)
     else:
-        plan = S.ShardPlan(W, H, world, args.side)
-    sizes, maxn = plan.sizes, plan.max_size
-    tiles = E.tiles_array(plan.tiles[rank]) if world > 1 else E.tiles_array([[0, 0, W - 1, H - 1]])
+        plan = S.ShardPlan(W, H, pw, args.side)
+    sizes = plan.sizes
+    if pw > 1 or args.single_tiles == "cost":
+        tiles = E.tiles_array(plan.tiles[pr])
+    else:
+        tiles = E.tiles_array([[0, 0, W - 1, H - 1]])
     S_, F_ = max(1, args.streams), args.frames_per_launch
     streams = [torch.cuda.Stream(dev) for _ in range(S_)]
-    npf = W * H if world == 1 else maxn  # output elements per frame (stride between frames)
-    # per stream slot: [F framebuffers][F ray_casts] (u32 each) and a traced-ray accumulator
-    outbuf = [torch.zeros(2 * F_ * npf, dtype=torch.int32, device=dev) for _ in range(S_)]
-    traced = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
+    own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
+    npx = W * H
     on_host = world > 1 and backend != "nccl"
-    images = None
-    if world > 1 and rank == 0:
-        big = [torch.zeros(world * 2 * F_ * maxn, dtype=torch.int32, device="cpu" if on_host else dev)
-               for _ in range(S_)]
-        gather = [list(b_.chunk(world)) for b_ in big]
-        dst_idx = torch.from_numpy(frame_assembly(plan, F_, world)).to(dev)
-        images = [torch.zeros(2 * F_ * (W * H + 1), dtype=torch.int32, device=dev) for _ in range(S_)]
-        staging = torch.zeros(world * 2 * F_ * maxn, dtype=torch.int32, device=dev) if on_host else None
-    layout = E.ATR_LAYOUT_IMAGE if world == 1 else E.ATR_LAYOUT_PACKED
+    traced = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
+    # per stream slot: F framebuffers and F ray_casts images (u32), frames back to back
+    casts = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
+    if pw == 1:
+        fbs = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
+    else:
+        # N > 1: rank r's packed frames go to rank 0 by exact-size send/recv into one buffer per
+        # slot holding every rank's F frames back to back (shard.frame_offsets); rank 0 renders
+        # its own block in place. The per-pixel ray_casts stay on their rank: each rank reduces
+        # them to per-tile sums (the reference's per-tile counters) and those are summed on rank 0.
+        off = S.frame_offsets(plan, F_)
+        ngrid = S.grid_tile_count(plan)
+        tids = torch.from_numpy(S.tile_ids(plan, pr)).to(dev)
+        tcasts = [torch.zeros(F_, max(1, len(tids)), dtype=torch.int64, device=dev) for _ in range(S_)]
+        tsum = [torch.zeros(F_, ngrid, dtype=torch.int64, device="cpu" if on_host else dev) for _ in range(S_)]
+        if rank == 0 and not sim:
+            big = [torch.zeros(F_ * npx, dtype=torch.int32, device="cpu" if on_host else dev) for _ in range(S_)]
+            dst_idx = torch.from_numpy(S.frames_assembly_index(plan, F_)).to(dev)
+            images = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
+            staging = torch.zeros(F_ * npx, dtype=torch.int32, device=dev) if on_host else None
+            fbs = [b_[off[0]:off[0] + F_ * own] if not on_host else torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev)
+                   for b_ in big]
+        else:
+            fbs = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
+    layout = E.ATR_LAYOUT_IMAGE if pw == 1 else E.ATR_LAYOUT_PACKED
 
-    def frame_of(q, nf_cap=F_):
-        base = outbuf[q].data_ptr()
-        return E.atr_frame(layout, base, None, None, None, base + 4 * nf_cap * npf, traced[q].data_ptr())
+    def frame_of(q):
+        return E.atr_frame(layout, fbs[q].data_ptr(), None, None, None, casts[q].data_ptr(), traced[q].data_ptr())
 
     pending = {}
 
     def image_views(q, f):
-        """(framebuffer, ray_casts) of frame f of stream slot q as (H*W,) views."""
-        if world == 1:
-            b = outbuf[q]
-            return b[f * npf:(f + 1) * npf], b[(F_ + f) * npf:(F_ + f + 1) * npf]
-        npx = W * H + 1
-        im = images[q]
-        return im[f * npx:f * npx + W * H], im[(F_ + f) * npx:(F_ + f) * npx + W * H]
+        """(framebuffer, ray_casts or None) of frame f of stream slot q: (H*W,) views; at N > 1
+        the ray_casts are the reduced per-tile sums (ngrid,)."""
+        if pw == 1:
+            return fbs[q][f * npx:(f + 1) * npx], casts[q][f * npx:(f + 1) * npx]
+        if sim:
+            return None, tsum[q][f]
+        return images[q][f * npx:(f + 1) * npx], tsum[q][f]
 
     def assemble(j):
-        """Launch j's gather done (its stream waits on it); rank 0 scatters every rank's packed
+        """Launch j's exchange done (its stream waits on it); rank 0 scatters every rank's packed
         frames into that slot's images, on the launch's stream."""
-        q, work = pending.pop(j)
+        q, works = pending.pop(j)
         if world == 1:
             return
         with torch.cuda.stream(streams[q]):
-            if work is not None:
-                work.wait()
+            for w_ in works:
+                w_.wait()
             if rank == 0:
                 src = big[q]
                 if on_host:
@@ -448,16 +476,33 @@ def run(args):
         if j - S_ in pending:
             assemble(j - S_)  # before this slot's buffers are reused
         fr = [cams[(k0 + f) % n_orbit] for f in range(nf)]
-        eng.render_start_cameras(fr, tiles, frame_of(q), npf, SEED, stream=streams[q].cuda_stream, variant=variant)
-        if world > 1:
+        eng.render_start_cameras(fr, tiles, frame_of(q), own, SEED, stream=streams[q].cuda_stream, variant=variant)
+        if pw > 1:
             with torch.cuda.stream(streams[q]):
-                buf = outbuf[q]
+                ts = tsum[q]
+                ts.zero_()
+                if own:  # the reference's per-tile counters of this rank's tiles, scattered into the grid
+                    eng.packed_tile_ray_casts(tiles, W, H, casts[q].data_ptr(), nf, own, tcasts[q].data_ptr(),
+                                              stream=streams[q].cuda_stream)
+                    part = tcasts[q][:, :len(tids)]
+                    if on_host:
+                        ts.index_copy_(1, tids.cpu(), part.cpu())
+                    else:
+                        ts.index_copy_(1, tids, part)
+                if sim:
+                    pending[j] = (q, [])
+                    return
+                send = fbs[q]
                 if on_host:
                     torch.cuda.synchronize()
-                    buf = buf.cpu()
-                pending[j] = (q, dist.gather(buf, gather[q] if rank == 0 else None, dst=0, async_op=True))
+                    send = send.cpu()
+                    if rank == 0:
+                        big[q][off[0]:off[0] + nf * own] = send[:nf * own]
+                works = S.gather_frames(send, big[q] if rank == 0 else None, plan, rank, nf, dist)
+                works.append(dist.reduce(ts, dst=0, async_op=True))
+                pending[j] = (q, works)
         else:
-            pending[j] = (q, None)
+            pending[j] = (q, [])
 
     def run_frames(k0, k, on_launch=None):
         j0 = 0
@@ -474,9 +519,11 @@ def run(args):
     # setup, not warmup: one small launch on every stream (a stream's first launch pays its
     # hardware-queue setup, ~ms) so the timed region does not depend on W reaching every stream
     for q in range(S_):
-        eng.render_start_cameras([cams[0]], tiles, frame_of(q), npf, SEED, stream=streams[q].cuda_stream,
+        eng.render_start_cameras([cams[0]], tiles, frame_of(q), own, SEED, stream=streams[q].cuda_stream,
                                  variant=variant)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     run_frames(0, args.warmup)
     torch.cuda.synchronize()
     for t_ in traced:
@@ -501,11 +548,14 @@ def run(args):
     rays_total = int(rays.item())
 
     # ---- check (rank 0): the last S x F frames in the slots against one-launch full-frame renders
+    # (framebuffer per pixel; ray_casts per pixel at N = 1, per shard tile at N > 1)
     check = None
     casts_total = None
     if rank == 0:
         ref = torch.zeros(W * H, dtype=torch.int32, device=dev)
         refc = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        if pw > 1 and not sim:
+            full_tiles = torch.from_numpy(S.pixel_tiles(W, H, args.side)).to(dev)
         sizes_l = launch_sizes(args.steps, F_, S_)
         k0 = args.warmup
         last = {}
@@ -518,12 +568,17 @@ def run(args):
             for f in range(nf):
                 fb, cs = image_views(q, f)
                 casts_total += int(cs.to(torch.int64).sum().item())
-                if args.check:
+                if args.check and not sim:
                     fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, ref.data_ptr(), None, None, None, refc.data_ptr(), None)
                     eng.render_start(cams[(kk + f) % n_orbit], [[0, 0, W - 1, H - 1]], fr, SEED,
                                      stream=torch.cuda.current_stream(dev).cuda_stream)
                     torch.cuda.synchronize()
-                    mism += int((ref != fb).sum().item()) + int((refc != cs).sum().item())
+                    mism += int((ref != fb).sum().item())
+                    if world == 1:
+                        mism += int((refc != cs).sum().item())
+                    else:  # every shard tile's ray_casts sum (a mismatching tile counts as one)
+                        want = torch.zeros(ngrid, dtype=torch.int64, device=dev).index_add_(0, full_tiles, refc.to(torch.int64))
+                        mism += int((want.cpu() != cs.cpu()).sum().item())
         check = mism if args.check else None
         casts_frames = sum(nf for _, nf in last.values())
 
@@ -559,10 +614,12 @@ def run(args):
                                       f"{'octree' if use_tree else 'brute-force'}",
                           "rays_per_step": round(rays_total / args.steps), "shard_tile": args.side,
                           "parallelism": f"tiles{world}", "kernel": args.variant,
-                          "plan": args.plan if world > 1 else "single",
+                          "plan": (f"{args.plan}/{args.tile_order}" if pw > 1 else
+                                   "single" if args.single_tiles == "frame" else f"single/{args.tile_order}"),
                           "streams": args.streams, "frames_per_launch": F_,
                           "launches": launch_sizes(args.steps, F_, S_),
                           "shard_pixels": [int(x) for x in sizes]},
+               **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange"}} if sim else {}),
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
         if check is not None:
             out["check_mismatched_pixels"] = check

@@ -251,6 +251,15 @@ int atr_unpack(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t widt
    -> the reference's RenderTile::ray_casts (renderer.h:11-15); out is a device int64 array. */
 int atr_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width,
                        const uint32_t* ray_casts_image, int64_t* out, void* stream);
+/* Per-tile sums of a PACKED ray_casts buffer holding `nframes` frames (frame f at f *
+   frame_stride elements) rendered with these tiles at width x height -- the reference's
+   RenderTile::ray_casts (renderer.h:11-15, summed at renderer.cpp:465-468) for a shard's tiles
+   without an IMAGE copy: out[f * ntiles + i] = sum over the pixels of tile i (a pixel of
+   overlapping tiles counts in the first tile holding it: the packed layout traces it once).
+   Asynchronous on `stream`; out is a device int64 array, zeroed here. */
+int atr_packed_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width,
+                              int32_t height, const uint32_t* packed_ray_casts, int32_t nframes,
+                              int64_t frame_stride, int64_t* out, void* stream);
 /* wait_for_render_from_camera_to_finish: 1 = still running after timeout_ms, 0 = done,
    <0 = error. tiles_done (optional) = tiles of the last render known complete (progress). */
 int atr_render_wait(atr_ctx* ctx, uint32_t timeout_ms, int32_t* tiles_done);

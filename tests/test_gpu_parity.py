@@ -157,6 +157,39 @@ def test_reference_tiles_and_ray_cast_counts(eng):
     assert per.cpu().numpy().tolist() == want
 
 
+@pytest.mark.parametrize("kind", ["shard", "reference"])
+def test_packed_tile_ray_casts(eng, kind):
+    """atr_packed_tile_ray_casts (the multi-GPU bench's per-tile counters): per-tile sums of a
+    PACKED multi-frame ray_casts buffer equal the sums of the golden per-pixel ray_casts over each
+    tile's pixels -- shard tiles (disjoint), and the reference's overlapping tiles, where a pixel
+    counts in the first tile holding it (the packed layout traces it once)."""
+    name = "monkey_320x180_s4_b5"
+    g = GOLD["render"][name]
+    upload(eng, "Monkey", True)
+    W, H = g["W"], g["H"]
+    cam = E.camera(W, H, g["spp"], g["bounces"])
+    tiles = E.make_shard_tiles(W, H, 32, 1, 3) if kind == "shard" else E.make_tiles(W, H, 8)
+    o = run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED)
+    n = E.packed_size(tiles)
+    F, stride = 3, n + 11
+    casts = torch.full((F * stride,), 5, dtype=torch.int32, device="cuda")
+    for f in range(F):  # frame f holds the render's ray_casts + f per pixel
+        casts[f * stride:f * stride + n] = torch.from_numpy(o["casts"].view(np.int32) + f).cuda()
+    out = torch.full((F * len(tiles),), -3, dtype=torch.int64, device="cuda")
+    eng.packed_tile_ray_casts(tiles, W, H, casts.data_ptr(), F, stride, out.data_ptr(),
+                              stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _, _, gcasts = render(name)
+    owner = np.full((H, W), -1, np.int64)
+    for k, (x0, y0, x1, y1) in enumerate(tiles):
+        blk = owner[y0:y1 + 1, x0:x1 + 1]
+        blk[blk < 0] = k
+    got = out.cpu().numpy().reshape(F, len(tiles))
+    for f in range(F):
+        want = [int((gcasts.astype(np.int64) + f)[owner == k].sum()) for k in range(len(tiles))]
+        assert got[f].tolist() == want
+
+
 def test_renderer_api_start_wait(eng):
     """renderer.h's start/wait pair over the engine, app-scene materials (app.cpp:91-131)."""
     from atray_amd import renderer as R
