@@ -58,6 +58,7 @@ struct BlockSet {
     DevBuf dev;
     DevBuf dev_tiles;
     DevBuf dev_pix;  // pixel index per packed slot (wavefront schedule)
+    uint32_t cplan_gen = 0;  // the ctx's cell plan this set was built with
     DevBuf dev_tile;  // owning tile per packed slot (atr_packed_tile_ray_casts; built on first use)
     bool tile_ready = false;
     int64_t packed_pixels = 0;
@@ -86,7 +87,7 @@ uint64_t morton2(uint32_t x, uint32_t y) {
 // first_emit > 0: the pixels of tiles[0, first_emit) are left out (they belong to an earlier
 // launch of a progressive render) and only tiles[first_emit, ntiles) emit blocks.
 void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, std::vector<DBlock>& out,
-                  int64_t& npix, int32_t first_emit = 0) {
+                  int64_t& npix, int32_t first_emit = 0, const uint8_t* cplan = nullptr) {
     const int32_t cw = (W + 7) / 8, ch = (H + 7) / 8;
     std::vector<uint64_t> cell(size_t(cw) * size_t(ch), 0), done(first_emit > 0 ? cell.size() : 0, 0);
     // tile order decides the block order: cells are emitted tile by tile (first owner wins)
@@ -131,15 +132,26 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     out.reserve(order.size());
     npix = 0;
     for (int32_t ci : order) {
-        DBlock b;
-        std::memset(&b, 0, sizeof(b));
-        b.x0 = (ci % cw) * 8;
-        b.y0 = (ci / cw) * 8;
-        b.mask_lo = uint32_t(cell[size_t(ci)]);
-        b.mask_hi = uint32_t(cell[size_t(ci)] >> 32);
-        b.out_base = int32_t(npix);
-        npix += __builtin_popcountll(cell[size_t(ci)]);
-        out.push_back(b);
+        // cell plan (atr_set_cell_plan): a heavy cell is split into `parts` row bands, one wave
+        // each, emitted back to back in lane order (the packed slot order does not change)
+        const uint8_t pl = cplan ? cplan[ci] : 0;
+        const int parts = (pl & 0xF) >= 2 ? (pl & 0xF) : 1;
+        const uint64_t cm = cell[size_t(ci)];
+        for (int k = 0; k < parts; ++k) {
+            const int rows = 8 / parts;
+            const uint64_t band = parts == 1 ? ~uint64_t(0) : ((uint64_t(1) << (8 * rows)) - 1) << (8 * rows * k);
+            const uint64_t m = cm & band;
+            if (!m) continue;
+            DBlock b;
+            std::memset(&b, 0, sizeof(b));
+            b.x0 = (ci % cw) * 8;
+            b.y0 = (ci / cw) * 8;
+            b.mask_lo = uint32_t(m);
+            b.mask_hi = uint32_t(m >> 32);
+            b.out_base = int32_t(npix);
+            npix += __builtin_popcountll(m);
+            out.push_back(b);
+        }
     }
 }
 
@@ -208,6 +220,11 @@ struct atr_ctx {
     int32_t max_nodes = 0, max_depth = 0, nmodels = 0, max_inner = 0;
     int cluster_size = 16;     // primitives per leaf cluster (ATR_CLUSTER_SIZE overrides, 1..16)
     int64_t nclusters = 0;
+    // per-cell plan (atr_set_cell_plan) for images of cplan_w x cplan_h; cplan_gen invalidates
+    // the block cache
+    std::vector<uint8_t> cplan;
+    int32_t cplan_w = 0, cplan_h = 0;
+    uint32_t cplan_gen = 0;
     static constexpr int kBlockSlots = 24;  // tile-list cache: own render + one unpack per rank
     BlockSet blocks[kBlockSlots];
     uint64_t block_use[kBlockSlots] = {};
@@ -362,7 +379,7 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     for (int i = 0; i < atr_ctx::kBlockSlots; ++i) {
         BlockSet& b = c->blocks[i];
         if (b.width == W && b.height == H && int32_t(b.tiles.size()) == ntiles && b.dev.p &&
-            (ntiles == 0 || std::memcmp(b.tiles.data(), tiles, sizeof(atr_tile) * size_t(ntiles)) == 0)) {
+            b.cplan_gen == c->cplan_gen && (ntiles == 0 || std::memcmp(b.tiles.data(), tiles, sizeof(atr_tile) * size_t(ntiles)) == 0)) {
             c->block_use[i] = ++c->use_clock;
             return &b;
         }
@@ -380,7 +397,9 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     b.tile_ready = false;
     b.width = W;
     b.height = H;
-    build_blocks(tiles, ntiles, W, H, b.host, b.packed_pixels);
+    b.cplan_gen = c->cplan_gen;
+    const bool planned = !c->cplan.empty() && c->cplan_w == W && c->cplan_h == H;
+    build_blocks(tiles, ntiles, W, H, b.host, b.packed_pixels, 0, planned ? c->cplan.data() : nullptr);
     const size_t need = std::max<size_t>(b.host.size() * sizeof(DBlock), 32);
     if (b.dev.n < need) {
         if (b.dev.p) (void)hipFree(b.dev.p);
@@ -1606,6 +1625,64 @@ int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles,
     HIPCHK(atr_launch_packed_tile_casts(static_cast<const int32_t*>(bs->dev_tile.p), n, casts, frame_stride, nframes,
                                         ntiles, reinterpret_cast<unsigned long long*>(out), s));
     HIPCHK(note_launch(c, s, bs));
+    return ATR_OK;
+}
+
+int atr_set_cell_plan(atr_ctx* c, int32_t width, int32_t height, const uint8_t* plan) {
+    if (!c || (plan && (width <= 0 || height <= 0))) return ATR_E_INVALID;
+    const int32_t cw = (width + 7) / 8, ch = (height + 7) / 8;
+    if (plan) {
+        for (size_t i = 0; i < size_t(cw) * size_t(ch); ++i) {
+            const int p = plan[i] & 0xF;
+            if ((plan[i] & 0xF0) || !(p == 0 || p == 1 || p == 2 || p == 4 || p == 8)) return ATR_E_INVALID;
+        }
+        c->cplan.assign(plan, plan + size_t(cw) * size_t(ch));
+        c->cplan_w = width;
+        c->cplan_h = height;
+    } else {
+        c->cplan.clear();
+        c->cplan_w = c->cplan_h = 0;
+    }
+    ++c->cplan_gen;  // cached block lists are rebuilt on their next use
+    return ATR_OK;
+}
+
+int atr_render_cell_costs(atr_ctx* c, const atr_camera* cam, uint64_t seed, int32_t variant, int64_t* out) {
+    if (!c || !cam || !out || cam->width <= 0 || cam->height <= 0) return ATR_E_INVALID;
+    if (!c->d_scene) return ATR_E_NOSCENE;
+    HIPCHK(hipSetDevice(c->device));
+    const int32_t cw = (cam->width + 7) / 8, ch = (cam->height + 7) / 8;
+    const atr_tile full = {0, 0, cam->width - 1, cam->height - 1};
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, &full, 1, cam->width, cam->height, rc);
+    if (!bs) return rc;
+    const size_t nb = bs->host.size();
+    DevTmp fb;
+    DevTmp cost;
+    HIPCHK(hipMalloc(&fb.p, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
+    HIPCHK(hipMalloc(&cost.p, std::max<size_t>(1, nb) * sizeof(unsigned long long)));
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.cam = *cam;
+    P.scene = c->d_scene;
+    P.seed = seed;
+    P.blocks = static_cast<const DBlock*>(bs->dev.p);
+    P.nblocks = int32_t(nb);
+    P.layout = ATR_LAYOUT_PACKED;
+    P.framebuffer = static_cast<uint32_t*>(fb.p);
+    P.error_flag = c->d_error;
+    P.block_cost = static_cast<unsigned long long*>(cost.p);
+    P.xcd_chunk = xcd_chunk();
+    set_hybrid(P);
+    if (variant == ATR_KERNEL_PERSIST || variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;  // cell kernels only
+    const int sched = auto_sched(variant, *cam);
+    HIPCHK(atr_launch_render(P, sched, nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(nb);
+    if (nb) HIPCHK(hipMemcpy(h.data(), cost.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < size_t(cw) * size_t(ch); ++i) out[i] = 0;
+    for (size_t k = 0; k < nb; ++k)  // a split cell's waves add up
+        out[size_t(bs->host[k].y0 / 8) * size_t(cw) + size_t(bs->host[k].x0 / 8)] += int64_t(h[k]);
     return ATR_OK;
 }
 

@@ -96,7 +96,7 @@ EXPORTS = [
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
-    "atr_mesh_export", "atr_packed_tile_ray_casts",
+    "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
 ]
 
 _lib = None
@@ -149,6 +149,8 @@ def lib():
         "atr_unpack": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_packed_tile_ray_casts": ([vp, vp, i32, i32, i32, vp, i32, i64, vp, vp], C.c_int),
+        "atr_set_cell_plan": ([vp, i32, i32, vp], C.c_int),
+        "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
         "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
         "atr_render_start_progressive": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32, i32],
                                          C.c_int),
@@ -498,6 +500,22 @@ class Engine:
                                               C.c_void_p(casts_ptr), int(nframes), int(frame_stride),
                                               C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None),
               "packed tile casts")
+
+    def set_cell_plan(self, width, height, plan=None):
+        """Per-8x8-cell split/priority bytes (atr_set_cell_plan); None clears."""
+        if plan is None:
+            check(lib().atr_set_cell_plan(self.h, int(width), int(height), None), "cell plan")
+            return
+        plan = np.ascontiguousarray(plan, np.uint8)
+        assert plan.size == ((width + 7) // 8) * ((height + 7) // 8)
+        check(lib().atr_set_cell_plan(self.h, int(width), int(height), plan.ctypes.data), "cell plan")
+
+    def cell_costs(self, cam, seed, variant=ATR_KERNEL_AUTO):
+        """Shader clocks per 8x8 cell of one full-frame render ((H+7)/8, (W+7)/8)."""
+        out = np.zeros(((cam.height + 7) // 8) * ((cam.width + 7) // 8), np.int64)
+        check(lib().atr_render_cell_costs(self.h, C.byref(cam), C.c_uint64(seed), int(variant), out.ctypes.data),
+              "cell costs")
+        return out.reshape((cam.height + 7) // 8, (cam.width + 7) // 8)
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

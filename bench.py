@@ -232,6 +232,9 @@ def main():
                     help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
     ap.add_argument("--calib-frames", type=int, default=3,
                     help="cost plan: per-tile costs summed over this many of the run's frames (one calibration render each)")
+    ap.add_argument("--cell-split", default="",
+                    help="P:FRAC -- the FRAC most expensive 8x8 cells (measured on the calibration frames) are "
+                         "traced by P waves each (atr_set_cell_plan; scheduling only, same outputs)")
     ap.add_argument("--tile-order", default="cost", choices=["cost", "grid"],
                     help="N>1 (and --single-tiles cost): each rank's tiles heaviest first (default) or in grid order")
     ap.add_argument("--single-tiles", default="frame", choices=["frame", "cost"],
@@ -407,6 +410,17 @@ def run(args):
     else:
         plan = S.ShardPlan(W, H, pw, args.side)
     sizes = plan.sizes
+    cell_split = None
+    if args.cell_split:  # the heaviest cells of the run's calibration frames, split over P waves
+        parts, frac = args.cell_split.split(":")
+        ks = sorted({args.warmup + (args.steps * i) // max(1, args.calib_frames) for i in range(args.calib_frames)})
+        cc = sum(eng.cell_costs(cams[k % n_orbit], SEED, variant) for k in ks)
+        nsplit = int(round(float(frac) * cc.size))
+        cplan = np.zeros(cc.size, np.uint8)
+        if nsplit > 0:
+            cplan[np.argsort(-cc.ravel(), kind="stable")[:nsplit]] = int(parts)
+        eng.set_cell_plan(W, H, cplan)
+        cell_split = {"parts": int(parts), "cells": nsplit, "of": int(cc.size)}
     if pw > 1 or args.single_tiles == "cost":
         tiles = E.tiles_array(plan.tiles[pr])
     else:
@@ -618,6 +632,7 @@ def run(args):
                                    "single" if args.single_tiles == "frame" else f"single/{args.tile_order}"),
                           "streams": args.streams, "frames_per_launch": F_,
                           "launches": launch_sizes(args.steps, F_, S_),
+                          "cell_split": cell_split,
                           "shard_pixels": [int(x) for x in sizes]},
                **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange"}} if sim else {}),
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}

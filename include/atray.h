@@ -260,6 +260,16 @@ int atr_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int3
 int atr_packed_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width,
                               int32_t height, const uint32_t* packed_ray_casts, int32_t nframes,
                               int64_t frame_stride, int64_t* out, void* stream);
+/* Per-cell launch plan for renders of width x height (NULL clears): one byte per 8x8 cell (row
+   major, ceil(W/8) x ceil(H/8)): the number of waves the cell is split into (0/1 = one, 2, 4 or
+   8 row bands: a heavy cell's rays then share their dealt leaf scans with 2-8x as many lanes and
+   its dependent chain shortens). Only scheduling changes: outputs and the PACKED slot order are
+   identical with any plan. */
+int atr_set_cell_plan(atr_ctx* ctx, int32_t width, int32_t height, const uint8_t* plan);
+/* Measured cost (shader clocks) of every 8x8 cell of a full-frame render of `cam` with `variant`
+   (cell kernels only): out has ceil(W/8) x ceil(H/8) entries, row major. Synchronous. */
+int atr_render_cell_costs(atr_ctx* ctx, const atr_camera* cam, uint64_t seed, int32_t variant,
+                          int64_t* out);
 /* wait_for_render_from_camera_to_finish: 1 = still running after timeout_ms, 0 = done,
    <0 = error. tiles_done (optional) = tiles of the last render known complete (progress). */
 int atr_render_wait(atr_ctx* ctx, uint32_t timeout_ms, int32_t* tiles_done);

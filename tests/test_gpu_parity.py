@@ -190,6 +190,36 @@ def test_packed_tile_ray_casts(eng, kind):
         assert got[f].tolist() == want
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_cell_plan_changes_no_output(eng, variant):
+    """atr_set_cell_plan: cells split over 2, 4 or 8 waves (the measured heaviest and some at
+    random) leave every output identical, image and packed layouts, primary and multi-bounce."""
+    upload(eng, "Dragon", True)
+    W, H = 480, 270
+    rng = np.random.default_rng(3)
+    try:
+        for spp, bounces in ((1, 1), (2, 3)):
+            cam = E.camera(W, H, spp, bounces)
+            tiles = E.make_shard_tiles(W, H, 64, 0, 2)
+            want = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
+                                                         variant=variant)]
+            cost = eng.cell_costs(E.camera(W, H), SEED).ravel()
+            plan = rng.choice(np.array([0, 1, 2, 4, 8], np.uint8), size=cost.size, p=[0.6, 0.1, 0.1, 0.1, 0.1])
+            plan[np.argsort(-cost)[:40]] = 4
+            eng.set_cell_plan(W, H, plan)
+            got = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
+                                                        variant=variant)]
+            eng.set_cell_plan(W, H, None)
+            for a, b in zip(want, got):
+                for k in ("fb", "face", "t", "casts", "rgb"):
+                    assert np.array_equal(np.asarray(a[k]).view(np.uint32), np.asarray(b[k]).view(np.uint32)), k
+                assert a["traced"] == b["traced"]
+    finally:
+        eng.set_cell_plan(W, H, None)
+    with pytest.raises(E.AtrError):
+        eng.set_cell_plan(W, H, np.full(((W + 7) // 8) * ((H + 7) // 8), 3, np.uint8))
+
+
 def test_renderer_api_start_wait(eng):
     """renderer.h's start/wait pair over the engine, app-scene materials (app.cpp:91-131)."""
     from atray_amd import renderer as R
