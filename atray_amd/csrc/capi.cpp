@@ -1521,10 +1521,17 @@ int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
         const auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
         if (uint32_t(el.count()) >= timeout_ms) {
             if (tiles_done && c->prog_active) {  // tiles of the leading groups already complete
-                for (size_t g = 0; g < c->prog_end.size(); ++g) {
+                size_t g = 0;
+                for (; g < c->prog_end.size(); ++g) {
                     const hipError_t qg = hipEventQuery(c->prog_ev[g]);
                     if (qg != hipSuccess) break;
                     *tiles_done = c->prog_end[g];
+                }
+                // every group finished since ev_done was queried: the render is done (ev_done
+                // follows the last group on the same stream), report it as done, not running
+                if (g == c->prog_end.size() && !c->prog_end.empty()) {
+                    HIPCHK(hipEventSynchronize(c->ev_done));
+                    break;
                 }
             }
             return 1;
