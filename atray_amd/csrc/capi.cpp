@@ -1351,9 +1351,11 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     return ATR_OK;
 }
 
-int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                        uint64_t seed, int32_t variant, int64_t out[10]) {
-    if (!c || !cam || !out || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+// One instrumented (COUNT) render; h = the 16 device counters (render.hip: [0..9] work counters,
+// [10..13] phase clocks).
+static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles, uint64_t seed,
+                        int32_t variant, unsigned long long h[16]) {
+    if (!c || !cam || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
     int rc = ATR_OK;
@@ -1362,8 +1364,8 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     DevTmp fb;
     DevTmp ctr;
     HIPCHK(hipMalloc(&fb.p, size_t(cam->width) * size_t(cam->height) * 4));
-    HIPCHK(hipMalloc(&ctr.p, 10 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(ctr.p, 0, 10 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&ctr.p, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctr.p, 0, 16 * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1378,9 +1380,27 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     const int sc = auto_sched(variant, *cam);
     HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
-    unsigned long long h[10];
-    HIPCHK(hipMemcpy(h, ctr.p, sizeof(h), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h, ctr.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return ATR_OK;
+}
+
+int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                        uint64_t seed, int32_t variant, int64_t out[10]) {
+    if (!out) return ATR_E_INVALID;
+    unsigned long long h[16];
+    const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
+    if (rc != ATR_OK) return rc;
     for (int k = 0; k < 10; ++k) out[k] = int64_t(h[k]);
+    return ATR_OK;
+}
+
+int atr_render_phase_clocks(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                            uint64_t seed, int32_t variant, int64_t out[4]) {
+    if (!out) return ATR_E_INVALID;
+    unsigned long long h[16];
+    const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
+    if (rc != ATR_OK) return rc;
+    for (int k = 0; k < 4; ++k) out[k] = int64_t(h[10 + k]);
     return ATR_OK;
 }
 

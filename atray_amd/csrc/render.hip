@@ -311,6 +311,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     uint32_t res_slot = 0xFFFFFFFFu;
     float res_t = kMaxFloat, res_u = 0.f, res_v = 0.f;
     for (;;) {
+        const uint64_t tc0 = COUNT ? clock64() : 0;
         if constexpr (UT) {  // the wave walks its passes together (traverse_pass_wave)
             if (__ballot(need)) {
                 LdsLeafBuf<K> lb;
@@ -342,6 +343,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             if (n < 0) { err = 1; done = true; }
             else { nb = n < K ? n : K; more = n > K; if (nb == 0) done = true; }
         }
+        if constexpr (COUNT) ct.t_pass += clock64() - tc0;
         if (__ballot(!done) == 0) break;
         // every live ray's current leaf: its clusters are this step's items
         int32_t leaf = -1;
@@ -370,6 +372,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
         }
         bool lp_imp = false;  // lane-private scan: this lane's leaf improved its hit
+        const uint64_t tc1 = COUNT ? clock64() : 0;
         if (!deal) {
             if (cn > 0) {
                 LeafHit lh;
@@ -383,6 +386,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 if (lh.improved) { lp_imp = true; res_t = lh.t; res_slot = lh.slot; res_u = lh.u; res_v = lh.v; }
             }
         }
+        if constexpr (COUNT) { if (!deal) ct.t_lp += clock64() - tc1; }
         int32_t carry = -1;
         for (uint32_t base = 0; deal && base < total; base += 64) {  // rounds of 64 items, wave-uniform
             s_mark[w][ln] = -1;
@@ -435,6 +439,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             }
             __builtin_amdgcn_wave_barrier();
         }
+        if constexpr (COUNT) { if (deal) ct.t_deal += clock64() - tc1; }
         if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
             bool imp = lp_imp;
             if (deal) {
@@ -800,6 +805,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     const bool active = (mask >> lane) & 1;
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
     const uint64_t clk0 = P.block_cost ? clock64() : 0;
+    const uint64_t clk1 = COUNT ? clock64() : 0;
     const uint64_t rt0 = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0;
     // per-frame cameras (atr_render_start_cameras): fidx is wave-uniform, so the camera comes from
     // the kernel argument with scalar loads
@@ -911,6 +917,13 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
             if (lane == 0 && x) atomicAdd(C + 8 + k, (unsigned long long)x);
+        }
+        // counters[10..13]: wave clocks in DFS passes, lane-private scans, dealt rounds, whole wave
+        if (lane == 0 && in_range) {
+            atomicAdd(C + 10, (unsigned long long)ct.t_pass);
+            atomicAdd(C + 11, (unsigned long long)ct.t_lp);
+            atomicAdd(C + 12, (unsigned long long)ct.t_deal);
+            atomicAdd(C + 13, (unsigned long long)(clock64() - clk1));
         }
     }
 }

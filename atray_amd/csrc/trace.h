@@ -21,6 +21,9 @@ namespace atr {
 struct Ctr {
     uint32_t box = 0, box_all = 0, tri = 0, leaf = 0, wave_tri = 0, pass = 0;
     uint32_t cbox = 0, screen = 0;  // clustered scan: cluster boxes tested, primitives screened
+    // wave clocks (s_memtime) in the FLAT/HYBRID scan's phases: DFS passes, lane-private leaf
+    // scans, dealt rounds (atr_render_phase_clocks)
+    uint64_t t_pass = 0, t_lp = 0, t_deal = 0;
 };
 
 struct Ray {

@@ -97,6 +97,7 @@ EXPORTS = [
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
+    "atr_render_phase_clocks",
 ]
 
 _lib = None
@@ -150,6 +151,7 @@ def lib():
         "atr_tile_ray_casts": ([vp, vp, i32, i32, vp, vp, vp], C.c_int),
         "atr_packed_tile_ray_casts": ([vp, vp, i32, i32, i32, vp, i32, i64, vp, vp], C.c_int),
         "atr_set_cell_plan": ([vp, i32, i32, vp], C.c_int),
+        "atr_render_phase_clocks": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
         "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
         "atr_render_start_progressive": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32, i32],
@@ -509,6 +511,14 @@ class Engine:
         plan = np.ascontiguousarray(plan, np.uint8)
         assert plan.size == ((width + 7) // 8) * ((height + 7) // 8)
         check(lib().atr_set_cell_plan(self.h, int(width), int(height), plan.ctypes.data), "cell plan")
+
+    def phase_clocks(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
+        """Wave clocks in DFS passes, lane-private scans, dealt rounds, whole waves (diagnostic)."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        out = (C.c_int64 * 4)()
+        check(lib().atr_render_phase_clocks(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed),
+                                            int(variant), out), "phase clocks")
+        return dict(zip(["pass", "lane_private", "dealt", "wave"], list(out)))
 
     def cell_costs(self, cam, seed, variant=ATR_KERNEL_AUTO):
         """Shader clocks per 8x8 cell of one full-frame render ((H+7)/8, (W+7)/8)."""

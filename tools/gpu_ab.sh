@@ -12,5 +12,5 @@ while IFS='|' read -r n e a; do
   [ -z "$n" ] && continue
   env $e timeout -k 10 200 python bench.py --no-pmc --no-cpu-baseline --no-prep $a > $O/$n.log 2>&1 || { tail -20 $O/$n.log; exit 1; }
   grep '^{' $O/$n.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('$n', d['value'], d['ms_per_step'], c['launches'], d['single_frame']['kernel_ms'])"
-done <<< "$AB"
+done <<< "${AB:-$(cat ${AB_FILE:-/dev/null})}"
 echo done
