@@ -1352,9 +1352,9 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
 }
 
 // One instrumented (COUNT) render; h = the 16 device counters (render.hip: [0..9] work counters,
-// [10..13] phase clocks).
+// [10..15] phase clocks, zero unless built with -DATR_PHASE_CLOCKS).
 static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles, uint64_t seed,
-                        int32_t variant, unsigned long long h[16]) {
+                        int32_t variant, unsigned long long h[20]) {
     if (!c || !cam || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
@@ -1364,8 +1364,8 @@ static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     DevTmp fb;
     DevTmp ctr;
     HIPCHK(hipMalloc(&fb.p, size_t(cam->width) * size_t(cam->height) * 4));
-    HIPCHK(hipMalloc(&ctr.p, 16 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(ctr.p, 0, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&ctr.p, 20 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctr.p, 0, 20 * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1377,17 +1377,19 @@ static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
     P.counters = static_cast<unsigned long long*>(ctr.p);
+    P.xcd_chunk = xcd_chunk();
+    set_hybrid(P);  // the product's HYBRID thresholds (the counts do not depend on them, the clocks do)
     const int sc = auto_sched(variant, *cam);
     HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(h, ctr.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h, ctr.p, 20 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;
 }
 
 int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         uint64_t seed, int32_t variant, int64_t out[10]) {
     if (!out) return ATR_E_INVALID;
-    unsigned long long h[16];
+    unsigned long long h[20];
     const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
     if (rc != ATR_OK) return rc;
     for (int k = 0; k < 10; ++k) out[k] = int64_t(h[k]);
@@ -1395,12 +1397,12 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
 }
 
 int atr_render_phase_clocks(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                            uint64_t seed, int32_t variant, int64_t out[4]) {
+                            uint64_t seed, int32_t variant, int64_t out[6]) {
     if (!out) return ATR_E_INVALID;
-    unsigned long long h[16];
+    unsigned long long h[20];
     const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
     if (rc != ATR_OK) return rc;
-    for (int k = 0; k < 4; ++k) out[k] = int64_t(h[10 + k]);
+    for (int k = 0; k < 6; ++k) out[k] = int64_t(h[10 + k]);
     return ATR_OK;
 }
 

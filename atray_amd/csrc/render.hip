@@ -251,6 +251,16 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
 // CLUSTER's, bit for bit.
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src); }
 
+// Phase clocks of the FLAT/HYBRID scans (atr_render_phase_clocks): compiled only into a diagnostic
+// build (make EXTRA=-DATR_PHASE_CLOCKS). In the product build the statements vanish; even
+// discarded under `if constexpr` they changed the product kernel's register allocation (3 spilled
+// VGPRs).
+#ifdef ATR_PHASE_CLOCKS
+#define ATR_PCLK(...) __VA_ARGS__
+#else
+#define ATR_PCLK(...)
+#endif
+
 // LDS of the FLAT/HYBRID scans (22.5 KB per 4-wave workgroup): the leaf order buffers (lane-private
 // columns), the per-owner best keys and hit records, the round's owner markers.
 struct FlatLds {
@@ -288,6 +298,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     auto& s_v = L.v;
     auto& s_mark = L.mark;
     const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    ATR_PCLK(uint64_t tcs = clock64());
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
@@ -311,7 +322,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     uint32_t res_slot = 0xFFFFFFFFu;
     float res_t = kMaxFloat, res_u = 0.f, res_v = 0.f;
     for (;;) {
-        const uint64_t tc0 = COUNT ? clock64() : 0;
+        ATR_PCLK(const uint64_t tc0 = clock64());
         if constexpr (UT) {  // the wave walks its passes together (traverse_pass_wave)
             if (__ballot(need)) {
                 LdsLeafBuf<K> lb;
@@ -343,7 +354,8 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             if (n < 0) { err = 1; done = true; }
             else { nb = n < K ? n : K; more = n > K; if (nb == 0) done = true; }
         }
-        if constexpr (COUNT) ct.t_pass += clock64() - tc0;
+        ATR_PCLK(const uint64_t tc2 = clock64());
+        ATR_PCLK(ct.t_pass += uint32_t(tc2 - tc0));
         if (__ballot(!done) == 0) break;
         // every live ray's current leaf: its clusters are this step's items
         int32_t leaf = -1;
@@ -372,7 +384,8 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
         }
         bool lp_imp = false;  // lane-private scan: this lane's leaf improved its hit
-        const uint64_t tc1 = COUNT ? clock64() : 0;
+        ATR_PCLK(const uint64_t tc1 = clock64());
+        ATR_PCLK(ct.t_prep += uint32_t(tc1 - tc2));
         if (!deal) {
             if (cn > 0) {
                 LeafHit lh;
@@ -386,7 +399,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 if (lh.improved) { lp_imp = true; res_t = lh.t; res_slot = lh.slot; res_u = lh.u; res_v = lh.v; }
             }
         }
-        if constexpr (COUNT) { if (!deal) ct.t_lp += clock64() - tc1; }
+        ATR_PCLK(if (!deal) ct.t_lp += uint32_t(clock64() - tc1));
         int32_t carry = -1;
         for (uint32_t base = 0; deal && base < total; base += 64) {  // rounds of 64 items, wave-uniform
             s_mark[w][ln] = -1;
@@ -439,7 +452,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             }
             __builtin_amdgcn_wave_barrier();
         }
-        if constexpr (COUNT) { if (deal) ct.t_deal += clock64() - tc1; }
+        ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
         if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
             bool imp = lp_imp;
             if (deal) {
@@ -471,6 +484,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         h.v = res_v;
         h.face = m.cface[res_slot];
     }
+    ATR_PCLK(ct.t_scan += uint32_t(clock64() - tcs));
 }
 
 // ------------------------------------------------------------------ TILE schedule
@@ -805,7 +819,8 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     const bool active = (mask >> lane) & 1;
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
     const uint64_t clk0 = P.block_cost ? clock64() : 0;
-    const uint64_t clk1 = COUNT ? clock64() : 0;
+    uint64_t clk1 = 0;
+    if constexpr (COUNT) clk1 = clock64();
     const uint64_t rt0 = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0;
     // per-frame cameras (atr_render_start_cameras): fidx is wave-uniform, so the camera comes from
     // the kernel argument with scalar loads
@@ -918,12 +933,15 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
             if (lane == 0 && x) atomicAdd(C + 8 + k, (unsigned long long)x);
         }
-        // counters[10..13]: wave clocks in DFS passes, lane-private scans, dealt rounds, whole wave
+        // counters[10..15]: wave clocks in DFS passes, lane-private scans, dealt rounds, whole
+        // wave, per-step preparation (leaf range, prefix sums, decision), whole FLAT/HYBRID scan
         if (lane == 0 && in_range) {
             atomicAdd(C + 10, (unsigned long long)ct.t_pass);
             atomicAdd(C + 11, (unsigned long long)ct.t_lp);
             atomicAdd(C + 12, (unsigned long long)ct.t_deal);
             atomicAdd(C + 13, (unsigned long long)(clock64() - clk1));
+            atomicAdd(C + 14, (unsigned long long)ct.t_prep);
+            atomicAdd(C + 15, (unsigned long long)ct.t_scan);
         }
     }
 }

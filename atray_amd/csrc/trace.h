@@ -23,7 +23,7 @@ struct Ctr {
     uint32_t cbox = 0, screen = 0;  // clustered scan: cluster boxes tested, primitives screened
     // wave clocks (s_memtime) in the FLAT/HYBRID scan's phases: DFS passes, lane-private leaf
     // scans, dealt rounds (atr_render_phase_clocks)
-    uint64_t t_pass = 0, t_lp = 0, t_deal = 0;
+    uint32_t t_pass = 0, t_lp = 0, t_deal = 0, t_prep = 0, t_scan = 0;  // per-wave deltas < 2^32
 };
 
 struct Ray {

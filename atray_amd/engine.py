@@ -515,10 +515,10 @@ class Engine:
     def phase_clocks(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
         """Wave clocks in DFS passes, lane-private scans, dealt rounds, whole waves (diagnostic)."""
         arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
-        out = (C.c_int64 * 4)()
+        out = (C.c_int64 * 6)()
         check(lib().atr_render_phase_clocks(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed),
                                             int(variant), out), "phase clocks")
-        return dict(zip(["pass", "lane_private", "dealt", "wave"], list(out)))
+        return dict(zip(["pass", "lane_private", "dealt", "wave", "step_prep", "scan"], list(out)))
 
     def cell_costs(self, cam, seed, variant=ATR_KERNEL_AUTO):
         """Shader clocks per 8x8 cell of one full-frame render ((H+7)/8, (W+7)/8)."""

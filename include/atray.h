@@ -234,10 +234,12 @@ int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* t
 int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         uint64_t seed, int32_t variant, int64_t counters_out[10]);
 /* Diagnostic: one instrumented render; out = wave clocks (s_memtime, summed over waves) spent in
-   DFS passes, lane-private leaf scans and dealt leaf rounds of the FLAT/HYBRID scans, and in the
-   whole wave. */
+   the FLAT/HYBRID scans' DFS passes, lane-private leaf scans, dealt leaf rounds, in the whole
+   wave, in each leaf step's preparation (leaf range, prefix sums, schedule decision), and in the
+   whole scan (tree query). The per-phase clocks are compiled only into a diagnostic build
+   (make EXTRA=-DATR_PHASE_CLOCKS); the product library reports the whole-wave clocks alone. */
 int atr_render_phase_clocks(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                            uint64_t seed, int32_t variant, int64_t out[4]);
+                            uint64_t seed, int32_t variant, int64_t out[6]);
 /* Diagnostic: one render of `tiles` recording, per 8x8 work block (block order), the wave's start
    and end on the 100 MHz device clock and its HW_ID | XCC_ID << 32. out = 3 u64 per block;
    with out == NULL (or cap too small) only *nblocks is set. */

@@ -2,7 +2,11 @@
 scans and dealt rounds (atr_render_phase_clocks, instrumented build) on Dragon 1920x1080, for the
 primary-ray frame (HYBRID) and a multi-bounce frame (FLAT).
 
-python tools/phase_probe.py [--spp 4]
+python tools/phase_probe.py [--spp 4]   (library built with make EXTRA=-DATR_PHASE_CLOCKS)
+
+Measured (c3 one frame, HYBRID): DFS passes 6%, lane-private scans 41%, dealt rounds 10%, step
+preparation 10%, whole tree query 69% of the wave clocks; FLAT at 4 spp x 5 bounces: passes 34%,
+dealt rounds 49%, lane-private 9%, tree queries 95%.
 """
 import argparse
 import json
@@ -35,7 +39,7 @@ def main():
         eng.phase_clocks(cam, tiles, SEED, var)  # warm
         p = eng.phase_clocks(cam, tiles, SEED, var)
         w = max(1, p["wave"])
-        out[name] = {**p, **{k + "_frac": round(p[k] / w, 3) for k in ("pass", "lane_private", "dealt")}}
+        out[name] = {**p, **{k + "_frac": round(p[k] / w, 3) for k in ("pass", "lane_private", "dealt", "step_prep", "scan")}}
         print(name, out[name], flush=True)
     print(json.dumps(out))
 
