@@ -235,6 +235,9 @@ def main():
     ap.add_argument("--cell-split", default="",
                     help="P:FRAC -- the FRAC most expensive 8x8 cells (measured on the calibration frames) are "
                          "traced by P waves each (atr_set_cell_plan; scheduling only, same outputs)")
+    ap.add_argument("--stream-priority", type=int, default=-1,
+                    help="1: stream 0 at the device's highest priority (its launch completes first, so at N > 1 "
+                         "its exchange overlaps the other launches' rendering); -1 (default) = on for N > 1")
     ap.add_argument("--tile-order", default="cost", choices=["cost", "grid"],
                     help="N>1 (and --single-tiles cost): each rank's tiles heaviest first (default) or in grid order")
     ap.add_argument("--single-tiles", default="frame", choices=["frame", "cost"],
@@ -426,7 +429,14 @@ def run(args):
     else:
         tiles = E.tiles_array([[0, 0, W - 1, H - 1]])
     S_, F_ = max(1, args.streams), args.frames_per_launch
-    streams = [torch.cuda.Stream(dev) for _ in range(S_)]
+    # --stream-priority: stream 0 at the device's highest priority, so its launch's workgroups are
+    # dispatched first and it completes early; the other streams' work fills its tail, and at
+    # N > 1 its exchange overlaps their rendering
+    if args.stream_priority < 0:
+        args.stream_priority = int(pw > 1)
+    hi_prio = torch.cuda.Stream.priority_range()[1] if args.stream_priority else 0
+    streams = [torch.cuda.Stream(dev, priority=hi_prio if q == 0 else 0) for q in range(S_)]
+    launch_ev = []  # (launch, event after its render) of the timed region
     own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
     npx = W * H
     on_host = world > 1 and backend != "nccl"
@@ -460,6 +470,7 @@ def run(args):
         return E.atr_frame(layout, fbs[q].data_ptr(), None, None, None, casts[q].data_ptr(), traced[q].data_ptr())
 
     pending = {}
+    timing = [False]
 
     def image_views(q, f):
         """(framebuffer, ray_casts or None) of frame f of stream slot q: (H*W,) views; at N > 1
@@ -491,6 +502,10 @@ def run(args):
             assemble(j - S_)  # before this slot's buffers are reused
         fr = [cams[(k0 + f) % n_orbit] for f in range(nf)]
         eng.render_start_cameras(fr, tiles, frame_of(q), own, SEED, stream=streams[q].cuda_stream, variant=variant)
+        if timing[0]:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(streams[q])
+            launch_ev.append(ev)
         if pw > 1:
             with torch.cuda.stream(streams[q]):
                 ts = tsum[q]
@@ -546,12 +561,17 @@ def run(args):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev0.record(streams[0])
+    timing[0] = True
     t0 = time.perf_counter()
     run_frames(args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timing[0] = False
+    launch_done = [round(ev0.elapsed_time(e), 3) for e in launch_ev]  # ms after the timed region's start
     rays = torch.stack(traced).sum().reshape(1)
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -632,6 +652,7 @@ def run(args):
                                    "single" if args.single_tiles == "frame" else f"single/{args.tile_order}"),
                           "streams": args.streams, "frames_per_launch": F_,
                           "launches": launch_sizes(args.steps, F_, S_),
+                          "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),
                           "cell_split": cell_split,
                           "shard_pixels": [int(x) for x in sizes]},
                **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange"}} if sim else {}),

@@ -11,6 +11,6 @@ fi
 while IFS='|' read -r n e a; do
   [ -z "$n" ] && continue
   env $e timeout -k 10 200 python bench.py --no-pmc --no-cpu-baseline --no-prep $a > $O/$n.log 2>&1 || { tail -20 $O/$n.log; exit 1; }
-  grep '^{' $O/$n.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('$n', d['value'], d['ms_per_step'], c['launches'], d['single_frame']['kernel_ms'])"
+  grep '^{' $O/$n.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('$n', d['value'], d['ms_per_step'], c['launches'], d['single_frame']['kernel_ms'], c.get('launch_render_done_ms'))"
 done <<< "${AB:-$(cat ${AB_FILE:-/dev/null})}"
 echo done
