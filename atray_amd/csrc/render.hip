@@ -284,7 +284,8 @@ __device__ __forceinline__ FlatLds& flat_lds() {
 // hyb_a / hyb_b). A leaf's result does not depend on how its clusters were visited (minimum
 // (t, leaf rank)), so the choice changes no output bit. LDSB: the DFS pass inserts straight
 // into the LDS columns (CLUSTER's LdsLeafBuf) instead of a register buffer copied after it.
-template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false, bool UT = false>
+template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false, bool UT = false,
+          bool NUV = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
@@ -396,7 +397,12 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 lh.improved = false;
                 for (uint32_t c = cf; c < cf + cn; ++c)
                     cluster_step<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1], lh, ct);
-                if (lh.improved) { lp_imp = true; res_t = lh.t; res_slot = lh.slot; res_u = lh.u; res_v = lh.v; }
+                if (lh.improved) {
+                    lp_imp = true;
+                    res_t = lh.t;
+                    res_slot = lh.slot;
+                    if constexpr (!NUV) { res_u = lh.u; res_v = lh.v; }
+                }
             }
         }
         ATR_PCLK(if (!deal) ct.t_lp += uint32_t(clock64() - tc1));
@@ -447,8 +453,10 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             __builtin_amdgcn_wave_barrier();
             if (lh.improved && s_key[w][own] == mine) {  // the round's winner for this owner
                 s_slot[w][own] = lh.slot;
-                s_u[w][own] = lh.u;
-                s_v[w][own] = lh.v;
+                if constexpr (!NUV) {  // NUV: primary-only frames, u and v feed no output
+                    s_u[w][own] = lh.u;
+                    s_v[w][own] = lh.v;
+                }
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -461,8 +469,10 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 if (imp) {
                     res_t = __uint_as_float(uint32_t(key >> 32));
                     res_slot = s_slot[w][ln];
-                    res_u = s_u[w][ln];
-                    res_v = s_v[w][ln];
+                    if constexpr (!NUV) {
+                        res_u = s_u[w][ln];
+                        res_v = s_v[w][ln];
+                    }
                 }
             }
             if (imp) {
@@ -664,7 +674,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (SCHED == SCHED_HYBRID)
                 // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
                 // bounces: FLAT's register buffer and paired candidate loads (measured)
-                tree_closest_flat<COUNT, true, PR, !PR, PR, PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                tree_closest_flat<COUNT, true, PR, !PR, PR, PR, PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
