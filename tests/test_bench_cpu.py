@@ -20,7 +20,7 @@ def _json_line(out):
     return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
