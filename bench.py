@@ -436,7 +436,7 @@ def run(args):
         args.stream_priority = int(pw > 1)
     hi_prio = torch.cuda.Stream.priority_range()[1] if args.stream_priority else 0
     streams = [torch.cuda.Stream(dev, priority=hi_prio if q == 0 else 0) for q in range(S_)]
-    launch_ev = []  # (launch, event after its render) of the timed region
+    launch_ev = []  # an event after each timed launch's render, in launch order
     own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
     npx = W * H
     on_host = world > 1 and backend != "nccl"
