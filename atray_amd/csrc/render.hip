@@ -251,6 +251,30 @@ __device__ __forceinline__ void tree_closest_wave(const Ray& r, const DModel& m,
 // CLUSTER's, bit for bit.
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src); }
 
+// Wave-wide inclusive scans on the DPP row network (GFX9 rows of 16 lanes: shifts by 1, 2, 4, 8
+// within a row, then the broadcasts of lanes 15 and 31 into the rows above): six dependent VALU
+// steps, where a __shfl_up step is an LDS permute (ds_bpermute) round trip. Lanes shifted in
+// from outside a row, and rows outside the mask, contribute the identity (`old`).
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xf, 0xf, false));  // row_shr:1
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xf, 0xf, false));  // row_shr:2
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xf, 0xf, false));  // row_shr:4
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xf, 0xf, false));  // row_shr:8
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ int32_t wave_incl_max(int32_t x) {
+    constexpr int32_t lo = -2147483647 - 1;
+    x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x118, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x142, 0xa, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
 // Phase clocks of the FLAT/HYBRID scans (atr_render_phase_clocks): compiled only into a diagnostic
 // build (make EXTRA=-DATR_PHASE_CLOCKS). In the product build the statements vanish; even
 // discarded under `if constexpr` they changed the product kernel's register allocation (3 spilled
@@ -368,20 +392,14 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             cn = cr.y;
             if constexpr (COUNT) { ct.leaf += 1; ct.cbox += cn; }
         }
-        uint32_t incl = cn;  // inclusive prefix sum over the lanes
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = uint32_t(__shfl_up(int(incl), off));
-            if (ln >= off) incl += t;
-        }
+        const uint32_t incl = wave_incl_add(cn);  // inclusive prefix sum over the lanes
         const uint32_t excl = incl - cn;
         const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
         s_key[w][ln] = kInit;
         bool deal = true;
         if constexpr (HYB) {
-            uint32_t mx = cn;  // the largest cluster count of the step (wave-uniform after the xor tree)
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off)));
+            // the largest cluster count of the step (counts are small: the signed max is exact)
+            const uint32_t mx = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
             deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
         }
         bool lp_imp = false;  // lane-private scan: this lane's leaf improved its hit
@@ -412,12 +430,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             __builtin_amdgcn_wave_barrier();
             if (cn > 0 && excl >= base && excl < base + 64u) s_mark[w][excl - base] = ln;
             __builtin_amdgcn_wave_barrier();
-            int32_t own = s_mark[w][ln];
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {  // latest owner starting at or before this lane
-                const int32_t t = __shfl_up(own, off);
-                if (ln >= off && t > own) own = t;
-            }
+            int32_t own = wave_incl_max(s_mark[w][ln]);  // latest owner starting at or before this lane
             if (own < 0) own = carry;
             carry = __builtin_amdgcn_readlane(own, 63);
             const uint32_t k = base + uint32_t(ln);
