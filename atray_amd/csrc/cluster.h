@@ -145,7 +145,12 @@ __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float
 template <bool COUNT, bool PAIR = false>
 __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
                                              LeafHit& h, Ctr& ct) {
-    const ScreenRay sr = screen_ray(r);
+    // the screen constants (7 values) are recomputed for every cluster from an opaque copy of the
+    // ray instead of being hoisted out of the scan loops and held through the passes and rounds:
+    // ~10 VALU per cluster for 7 VGPRs, what lets HYBRID run 6 waves/SIMD
+    Ray rr = r;
+    asm volatile("" : "+v"(rr.d.x), "+v"(rr.d.y), "+v"(rr.d.z), "+v"(rr.inv.x), "+v"(rr.inv.y), "+v"(rr.inv.z));
+    const ScreenRay sr = screen_ray(rr);
     float dlo, dhi;
     if (!cluster_pads(r, sr, lo, hi, h.t, dlo, dhi)) return;
     const uint32_t first = kMaxClusterSize * c;

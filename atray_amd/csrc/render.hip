@@ -1135,8 +1135,8 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     switch (sched) {
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
         case 6: launch_sched<atr::SCHED_FLAT>(P, count, prim, s); break;
-        case 7:  // primaries at 5 waves/SIMD (measured: DESIGN.md §4e)
-            if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 5>), g, b, 0, s, P);
+        case 7:  // primaries at 6 waves/SIMD (80 VGPRs; measured: DESIGN.md §4e)
+            if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 6>), g, b, 0, s, P);
             else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
             break;
         case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;
