@@ -975,6 +975,7 @@ ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCH
 ATR_INST4(SCHED_FLAT) ATR_INST4(SCHED_HYBRID)
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_HYBRID, false, true, 7>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, false, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, true, 6>(RenderParams);
@@ -1093,6 +1094,7 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
         const int o = sched - 80;
         if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 5>), g, b, 0, s, P);
         else if (!count && o == 6 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 6>), g, b, 0, s, P);
+        else if (!count && o == 7 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 7>), g, b, 0, s, P);
         else if (!count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, false, 5>), g, b, 0, s, P);
         else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
         return hipGetLastError();
