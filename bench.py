@@ -98,10 +98,12 @@ def cpu_share():
     return max(1, n)
 
 
-def pmc_traffic(args, kernel_name):
-    """HBM bytes per one-frame render launch from two rocprofv3 --pmc passes (FETCH_SIZE,
-    WRITE_SIZE) of a short child run of this benchmark. FETCH_SIZE is doubled (MI355X_MICROARCH.md,
-    HBM: gfx950 reports half the bytes of wide reads); both counters are in KB."""
+def pmc_traffic(args, kernel_name, frames):
+    """HBM bytes per render launch of `frames` frames (the timed launches' shape) from two
+    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a short child run of this benchmark that
+    renders one such launch; the rows of the largest render grid are that launch. FETCH_SIZE is
+    doubled (MI355X_MICROARCH.md, HBM: gfx950 reports half the bytes of wide reads); both counters
+    are in KB."""
     exe = "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
         return None, "rocprofv3 missing"
@@ -110,8 +112,8 @@ def pmc_traffic(args, kernel_name):
         d = os.path.join(ROOT, "gpurun_out", f"pmc_{ctr.lower()}")
         os.makedirs(d, exist_ok=True)
         cmd = [exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
-               "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-               "--frames-per-launch", "1", "--streams", "1", "--config", args.config, "--variant", args.variant,
+               "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(frames), "--warmup", "1",
+               "--frames-per-launch", str(frames), "--streams", "1", "--config", args.config, "--variant", args.variant,
                "--no-cpu-baseline", "--no-pmc", "--no-prep"]
         env = dict(os.environ)
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
@@ -121,7 +123,7 @@ def pmc_traffic(args, kernel_name):
                            stderr=subprocess.DEVNULL)
         except Exception as e:  # noqa: BLE001
             return None, f"rocprofv3 {ctr} failed: {e}"
-        vals = []
+        rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
@@ -129,9 +131,11 @@ def pmc_traffic(args, kernel_name):
                     # product launches only (not the instrumented COUNT build: <.., true, ..>)
                     if kernel_name in name and not re.search(kernel_name + r"<(\d+, )?true", name) \
                             and row.get("Counter_Name") == ctr:
-                        vals.append(float(row["Counter_Value"]))
-        if not vals:
+                        rows.append((int(row.get("Grid_Size") or 0), float(row["Counter_Value"])))
+        if not rows:
             return None, f"no {ctr} rows"
+        big = max(g for g, _ in rows)  # the `frames`-frame launch
+        vals = [v for g, v in rows if g == big]
         out[ctr] = sum(vals) / len(vals)
     return 2.0 * out["FETCH_SIZE"] * 1024.0 + out["WRITE_SIZE"] * 1024.0, "ok"
 
@@ -436,7 +440,7 @@ def run(args):
         args.stream_priority = int(pw > 1)
     hi_prio = torch.cuda.Stream.priority_range()[1] if args.stream_priority else 0
     streams = [torch.cuda.Stream(dev, priority=hi_prio if q == 0 else 0) for q in range(S_)]
-    launch_ev = []  # an event after each timed launch's render, in launch order
+    launch_ev = []  # per timed launch: (frames, event before its render, event after), launch order
     own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
     npx = W * H
     on_host = world > 1 and backend != "nccl"
@@ -501,11 +505,14 @@ def run(args):
         if j - S_ in pending:
             assemble(j - S_)  # before this slot's buffers are reused
         fr = [cams[(k0 + f) % n_orbit] for f in range(nf)]
+        if timing[0]:
+            ev_a = torch.cuda.Event(enable_timing=True)
+            ev_a.record(streams[q])
         eng.render_start_cameras(fr, tiles, frame_of(q), own, SEED, stream=streams[q].cuda_stream, variant=variant)
         if timing[0]:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record(streams[q])
-            launch_ev.append(ev)
+            launch_ev.append((nf, ev_a, ev))
         if pw > 1:
             with torch.cuda.stream(streams[q]):
                 ts = tsum[q]
@@ -571,8 +578,11 @@ def run(args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timing[0] = False
-    launch_done = [round(ev0.elapsed_time(e), 3) for e in launch_ev]  # ms after the timed region's start
+    launch_done = [round(ev0.elapsed_time(e), 3) for _, _, e in launch_ev]  # ms after the timed region's start
+    launch_ms = [a.elapsed_time(e) for _, a, e in launch_ev]  # each timed launch's render, on its stream
+    launch_frames = [nf for nf, _, _ in launch_ev]
     rays = torch.stack(traced).sum().reshape(1)
+    local_rays_per_frame = float(rays.item()) / max(1, args.steps)  # this rank's traced rays per frame
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -662,28 +672,37 @@ def run(args):
         n1 = live_ctr["n_rays"]
         out["single_frame"] = {"kernel_ms": round(kern_ms, 4), "mrays_s": round(n1 / kern_ms / 1e3, 1),
                                "camera": "app", "rays": n1, "variant": VARIANT_NAMES.get(roof_variant, roof_variant)}
-        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel_ms": round(kern_ms, 4)}
+        # roofline of the timed launches themselves: algorithmic bytes of each launch (its frames x
+        # this rank's rays per frame x bytes per ray) / that launch's duration (HIP events on its
+        # stream around it), averaged over the timed launches -- the same launches rocprofv3's
+        # kernel trace of this command lists
         clustered = args.variant in ("auto", "cl", "ps", "flat", "hyb")
         bpr = cluster_bytes_per_ray(live_ctr) if clustered else algorithmic_bytes_per_ray(live_ctr)
-        achieved = bpr * n1 / (kern_ms * 1e-3) / 1e9
-        roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "bytes_per_ray": round(bpr, 1), "rays_per_launch": n1,
-                     "model": "clustered scan, own work (DESIGN.md 6)" if clustered
-                     else "reference work (SURVEY.md 8(d))"})
+        per_launch = [bpr * nf * local_rays_per_frame / (ms * 1e-3) / 1e9 for nf, ms in zip(launch_frames, launch_ms)]
+        achieved = float(np.mean(per_launch))
+        sf_achieved = bpr * n1 / (kern_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel_ms": round(float(np.mean(launch_ms)), 4), "launch_ms": [round(x, 3) for x in launch_ms],
+                "frames_per_launch": launch_frames, "concurrent_launches": S_,
+                "rays_per_launch": round(float(np.mean(launch_frames)) * local_rays_per_frame),
+                "bytes_per_ray": round(bpr, 1),
+                "model": "clustered scan, own work (DESIGN.md 6)" if clustered else "reference work (SURVEY.md 8(d))",
+                "single_frame_launch": {"kernel_ms": round(kern_ms, 4), "achieved": round(sf_achieved, 1),
+                                        "frac": round(sf_achieved / HBM_PEAK_GBS, 4), "rays": n1}}
         gname = GOLDEN_COUNTERS.get(args.config)
         if gname:  # the reference algorithm's bytes for the same rays, at this kernel's speed
             with open(os.path.join(ROOT, "tests", "golden", "goldens.json")) as f:
                 ctr = json.load(f)["hits"][gname]["counters"]
             rbpr = algorithmic_bytes_per_ray(ctr)
             roof["ref_bytes_per_ray"] = round(rbpr, 1)
-            roof["ref_equivalent_GBs"] = round(rbpr * n1 / (kern_ms * 1e-3) / 1e9, 1)
+            roof["ref_equivalent_GBs"] = round(rbpr / bpr * achieved, 1)
         # AUTO: CLUSTER cells for primary-only renders, FLAT cells otherwise (both render_kernel)
         kname = "persist_kernel" if args.variant == "ps" else "render_kernel"
         roof["kernel"] = kname
         roof["variant"] = VARIANT_NAMES.get(roof_variant, roof_variant)
         if world == 1 and not args.no_pmc:
-            traffic, why = pmc_traffic(args, kname)
+            traffic, why = pmc_traffic(args, kname, int(max(launch_frames)))
             roof["traffic"] = traffic
             roof["traffic_note"] = why
         out["roofline"] = roof
