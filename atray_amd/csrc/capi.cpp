@@ -62,8 +62,9 @@ struct BlockSet {
     DevBuf dev_tile;  // owning tile per packed slot (atr_packed_tile_ray_casts; built on first use)
     bool tile_ready = false;
     int64_t packed_pixels = 0;
-    hipEvent_t ev = nullptr;  // recorded on the stream of every launch that reads this set
-    bool used = false;
+    // one event per stream that launched work reading this set, recorded after its latest such
+    // launch: before the set's buffers are rewritten or freed, every one of them is waited for
+    std::vector<std::pair<hipStream_t, hipEvent_t>> evs;
 };
 
 // Device scratch freed on every exit path.
@@ -72,12 +73,6 @@ struct DevTmp {
     ~DevTmp() { if (p) (void)hipFree(p); }
 };
 
-int32_t env_int(const char* name, int32_t dflt);
-// Cell order within a tile: 1 = Z curve (default), 0 = rows (ATR_BLOCK_ORDER overrides).
-int32_t block_order() {
-    static const int32_t v = env_int("ATR_BLOCK_ORDER", 1);
-    return v;
-}
 uint64_t morton2(uint32_t x, uint32_t y) {
     uint64_t r = 0;
     for (int i = 0; i < 16; ++i) r |= (uint64_t((x >> i) & 1u) << (2 * i)) | (uint64_t((y >> i) & 1u) << (2 * i + 1));
@@ -94,7 +89,6 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     std::vector<int32_t> order;
     order.reserve(cell.size());
     std::vector<uint8_t> seen(cell.size(), 0);
-    const bool morton = block_order() == 1;
     std::vector<int32_t> fresh;
     for (int32_t k = 0; k < ntiles; ++k) {
         atr_tile t = tiles[k];
@@ -122,8 +116,9 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
                 if (!seen[ci]) { seen[ci] = 1; fresh.push_back(int32_t(ci)); }
                 cell[ci] |= m;
             }
-        if (morton)  // the tile's cells along a Z curve: consecutive waves trace a 2D patch
-            std::stable_sort(fresh.begin(), fresh.end(), [cw](int32_t a, int32_t b) {
+        // the tile's cells along a Z curve (Morton order): consecutive waves trace a 2D patch and
+        // share its leaves in their XCD's L2
+        std::stable_sort(fresh.begin(), fresh.end(), [cw](int32_t a, int32_t b) {
                 return morton2(uint32_t(a % cw), uint32_t(a / cw)) < morton2(uint32_t(b % cw), uint32_t(b / cw));
             });
         order.insert(order.end(), fresh.begin(), fresh.end());
@@ -164,41 +159,22 @@ uint16_t half_of_int(int32_t v) {
     return uint16_t(sign | (uint32_t(e + 15) << 10) | ((m << (10 - e)) & 0x3FFu));
 }
 
-int32_t env_int(const char* name, int32_t dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
-// 8x8-cell schedules: workgroup chunks dealt round-robin to the XCDs (render.hip remap_xcd;
-// DESIGN.md §4c). ATR_XCD_CHUNK overrides (0 = one contiguous range per XCD).
-int32_t xcd_chunk() {
-    static const int32_t v = env_int("ATR_XCD_CHUNK", 16);
-    return v;
-}
-// Multi-frame cell launches: rotation of each frame's block list (render.hip), 1024 = frame f
-// starts f / frames into its list; ATR_FRAME_ROTATE overrides.
-int32_t frame_rotate() {
-    static const int32_t v = std::max(0, std::min(1024, env_int("ATR_FRAME_ROTATE", 0)));
-    return v;
-}
-// HYBRID: a step's leaves are dealt over the lanes in rounds when the largest cluster count
-// exceeds a x rounds + b (render.hip tree_closest_flat); ATR_HYB_A / ATR_HYB_B override.
-void set_hybrid(RenderParams& P) {
-    static const int32_t a = env_int("ATR_HYB_A", 2), b = env_int("ATR_HYB_B", 1);
-    P.hyb_a = a;
-    P.hyb_b = b;
-}
-// PERSIST: 8x8 cells per work-queue chunk (ATR_QCHUNK overrides).
-int32_t qchunk() {
-    static const int32_t v = std::max(1, env_int("ATR_QCHUNK", 16));
-    return v;
-}
 // load_model_data's pool size (OBJ_loader.cpp:298: one chunk per pool thread): the host's
-// hardware threads, at most 16 (ATR_PARSE_THREADS overrides).
+// hardware threads, at most 16.
 int32_t default_parse_threads() {
-    const int32_t e = env_int("ATR_PARSE_THREADS", 0);
-    if (e > 0) return e;
     const unsigned hw = std::thread::hardware_concurrency();
     return int32_t(std::max(1u, std::min(16u, hw)));
+}
+atr_tuning default_tuning() {
+    atr_tuning t;
+    std::memset(&t, 0, sizeof(t));
+    t.xcd_chunk = 16;      // chunks of 16 cells per XCD, interleaved
+    t.frame_rotate = 0;    // §4b: rotation measured slower
+    t.hybrid_a = 2;        // §4e: sweep optimum
+    t.hybrid_b = 1;
+    t.persist_chunk = 16;  // §4c
+    t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
+    return t;
 }
 constexpr int kSchedPersist = 8;
 constexpr int kQueueSlots = 32;             // queue-head sets in flight (ring)
@@ -218,7 +194,7 @@ struct atr_ctx {
     DScene* d_scene = nullptr;
     int64_t scene_bytes = 0;
     int32_t max_nodes = 0, max_depth = 0, nmodels = 0, max_inner = 0;
-    int cluster_size = 16;     // primitives per leaf cluster (ATR_CLUSTER_SIZE overrides, 1..16)
+    atr_tuning tune = default_tuning();  // atr_set_tuning
     int64_t nclusters = 0;
     // per-cell plan (atr_set_cell_plan) for images of cplan_w x cplan_h; cplan_gen invalidates
     // the block cache
@@ -261,6 +237,14 @@ struct atr_ctx {
 
 namespace {
 
+// Scheduling knobs of a context (atr_set_tuning); each launch copies them into RenderParams.
+void apply_tuning(const atr_ctx* c, RenderParams& P) {
+    P.xcd_chunk = c->tune.xcd_chunk;
+    P.frame_rotate = 0;
+    P.hyb_a = c->tune.hybrid_a;
+    P.hyb_b = c->tune.hybrid_b;
+}
+
 int dev_upload(atr_ctx* c, const void* src, size_t bytes, void** out) {
     DevBuf b;
     b.n = bytes ? bytes : 16;
@@ -278,30 +262,41 @@ int dev_upload(atr_ctx* c, const void* src, size_t bytes, void** out) {
     return ATR_OK;
 }
 
-// Record that a launch on stream s is in flight (one reusable event per stream).
-hipError_t note_launch(atr_ctx* c, hipStream_t s, BlockSet* bs) {
-    hipError_t e = hipSuccess;
-    if (bs) {
-        if (!bs->ev && (e = hipEventCreateWithFlags(&bs->ev, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventRecord(bs->ev, s)) != hipSuccess) return e;
-        bs->used = true;
-    }
-    for (auto& se : c->stream_ev)
+// Record on stream s, in a (stream, event) list, that work on s is in flight. Entries whose work
+// has completed are reused, so a caller that creates a stream per job does not grow the list.
+hipError_t note_stream(std::vector<std::pair<hipStream_t, hipEvent_t>>& list, hipStream_t s) {
+    for (auto& se : list)
         if (se.first == s) return hipEventRecord(se.second, s);
+    for (auto& se : list)
+        if (hipEventQuery(se.second) == hipSuccess) {  // finished: take over its event
+            se.first = s;
+            return hipEventRecord(se.second, s);
+        }
     hipEvent_t ev = nullptr;
+    hipError_t e;
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
-    c->stream_ev.emplace_back(s, ev);
+    list.emplace_back(s, ev);
     return hipEventRecord(ev, s);
 }
 
-// Wait for every launch of this context still in flight, on any stream.
-hipError_t wait_all(atr_ctx* c) {
-    for (auto& se : c->stream_ev) {
+// Wait for every entry of a list (all streams).
+hipError_t wait_list(const std::vector<std::pair<hipStream_t, hipEvent_t>>& list) {
+    for (const auto& se : list) {
         const hipError_t e = hipEventSynchronize(se.second);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
+
+// Record that a launch on stream s is in flight (and reads block set bs, if any).
+hipError_t note_launch(atr_ctx* c, hipStream_t s, BlockSet* bs) {
+    hipError_t e;
+    if (bs && (e = note_stream(bs->evs, s)) != hipSuccess) return e;
+    return note_stream(c->stream_ev, s);
+}
+
+// Wait for every launch of this context still in flight, on any stream.
+hipError_t wait_all(atr_ctx* c) { return wait_list(c->stream_ev); }
 
 // Carve the wavefront workspace for n path slots and a tree of `nodes` nodes.
 int wf_reserve(atr_ctx* c, int64_t n, int64_t nodes) {
@@ -387,11 +382,10 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     }
     BlockSet& b = c->blocks[lru];
     c->block_use[lru] = ++c->use_clock;
-    // the slot may still be read by an in-flight kernel of an earlier render, on any stream
-    if (b.used) {
-        const hipError_t e = hipEventSynchronize(b.ev);
+    // the slot may still be read by in-flight kernels of earlier renders, on several streams
+    {
+        const hipError_t e = wait_list(b.evs);
         if (e != hipSuccess) { rc = -(1000 + int(e)); return nullptr; }
-        b.used = false;
     }
     b.tiles.assign(tiles, tiles + ntiles);
     b.tile_ready = false;
@@ -468,7 +462,7 @@ int auto_sched(int32_t variant, const atr_camera& cam) {
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
 hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
     if (sched != kSchedPersist) {
-        if (!P.traced_rays || P.counters) return atr_launch_render(P, sched, s);
+        if (!P.traced_rays) return atr_launch_render(P, sched, s);
         // traced rays into a zeroed set of 64 spread counters, then one add to the caller's
         const int k = c->tnext;
         c->tnext = (k + 1) % kQueueSlots;
@@ -492,7 +486,7 @@ hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) 
     if (c->qused[k] && (e = hipStreamWaitEvent(s, c->qev[k], 0)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(q, 0, kQueueBytes, s)) != hipSuccess) return e;
     P.queue = q;
-    P.qchunk = qchunk();
+    P.qchunk = c->tune.persist_chunk;
     if ((e = atr_launch_persist(P, c->ncu, s)) != hipSuccess) return e;
     if ((e = hipEventRecord(c->qev[k], s)) != hipSuccess) return e;
     c->qused[k] = true;
@@ -774,6 +768,28 @@ int atr_create(int device, atr_ctx** out) {
     return ATR_OK;
 }
 
+void atr_default_tuning(atr_tuning* out) {
+    if (out) *out = default_tuning();
+}
+
+int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
+    if (!c || !t) return ATR_E_INVALID;
+    if (t->xcd_chunk < 0 || t->xcd_chunk > 4096 || t->frame_rotate < 0 || t->frame_rotate > 1024 ||
+        t->hybrid_a < -4096 || t->hybrid_a > 4096 || t->hybrid_b < -4096 || t->hybrid_b > 4096 ||
+        t->persist_chunk < 1 || t->persist_chunk > 4096 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize)
+        return ATR_E_INVALID;
+    for (int32_t r : t->reserved)
+        if (r) return ATR_E_INVALID;
+    c->tune = *t;
+    return ATR_OK;
+}
+
+int atr_get_tuning(atr_ctx* c, atr_tuning* out) {
+    if (!c || !out) return ATR_E_INVALID;
+    *out = c->tune;
+    return ATR_OK;
+}
+
 int atr_destroy(atr_ctx* c) {
     if (!c) return ATR_E_INVALID;
     (void)hipSetDevice(c->device);
@@ -784,7 +800,7 @@ int atr_destroy(atr_ctx* c) {
         if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
         if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
         if (b.dev_tile.p) (void)hipFree(b.dev_tile.p);
-        if (b.ev) (void)hipEventDestroy(b.ev);
+        for (auto& se : b.evs) (void)hipEventDestroy(se.second);
     }
     for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
     if (c->wf_mem.p) (void)hipFree(c->wf_mem.p);
@@ -842,10 +858,6 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
     c->max_depth = 0;
     c->max_inner = 0;
     c->nclusters = 0;
-    if (const char* e = std::getenv("ATR_CLUSTER_SIZE")) {
-        const int v = std::atoi(e);
-        if (v >= 1 && v <= kMaxClusterSize) c->cluster_size = v;
-    }
     for (int32_t i = 0; i < nmodels; ++i) {
         const atr_model& md = models[i];
         const HostMesh& M = md.mesh->m;
@@ -950,7 +962,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
             }
             {  // clustered copy of the leaf primitives
                 LeafClusters C;
-                if ((rc = leaf_clusters(T, c->cluster_size, C))) return rc;
+                if ((rc = leaf_clusters(T, c->tune.cluster_size, C))) return rc;
                 // every cluster owns kMaxClusterSize consecutive slots (its first slot is 16 c), so
                 // the record's last word can carry the screen normals' step instead
                 const size_t ncl = C.rec.size() / 8;
@@ -1209,8 +1221,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     P.counters = nullptr;
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);
+    apply_tuning(c, P);
     const int wave = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     HIPCHK(launch_render(c, P, wave, s));
@@ -1267,15 +1278,14 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
     P.ray_casts = fr->ray_casts;
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);
+    apply_tuning(c, P);
     const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
         P.nblocks = nb * nframes;
         P.frame_blocks = nb;
         P.frame_stride = frame_stride;
-        P.frame_rotate = frame_rotate();
+        P.frame_rotate = c->tune.frame_rotate;
         if (ncams > 1) {
             P.nfcam = ncams;
             for (int32_t f = 0; f < ncams; ++f) P.fcam[f] = cams[f];
@@ -1342,8 +1352,7 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
     P.wave_trace = static_cast<unsigned long long*>(tr.p);
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);
+    apply_tuning(c, P);
     const int ts = sched_of(variant);  // per-cell trace: 8x8-cell schedules only
     HIPCHK(atr_launch_render(P, ts == kSchedPersist ? 4 : ts, nullptr));
     HIPCHK(hipDeviceSynchronize());
@@ -1353,8 +1362,9 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
 
 // One instrumented (COUNT) render; h = the 16 device counters (render.hip: [0..9] work counters,
 // [10..15] phase clocks, zero unless built with -DATR_PHASE_CLOCKS).
+constexpr int kCounterSlots = 32;
 static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles, uint64_t seed,
-                        int32_t variant, unsigned long long h[20]) {
+                        int32_t variant, unsigned long long h[kCounterSlots]) {
     if (!c || !cam || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
@@ -1364,8 +1374,8 @@ static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     DevTmp fb;
     DevTmp ctr;
     HIPCHK(hipMalloc(&fb.p, size_t(cam->width) * size_t(cam->height) * 4));
-    HIPCHK(hipMalloc(&ctr.p, 20 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(ctr.p, 0, 20 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&ctr.p, kCounterSlots * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctr.p, 0, kCounterSlots * sizeof(unsigned long long)));
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1377,19 +1387,18 @@ static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
     P.counters = static_cast<unsigned long long*>(ctr.p);
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);  // the product's HYBRID thresholds (the counts do not depend on them, the clocks do)
+    apply_tuning(c, P);  // the product's HYBRID thresholds (the counts do not depend on them, the clocks do)
     const int sc = auto_sched(variant, *cam);
     HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(h, ctr.p, 20 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h, ctr.p, kCounterSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;
 }
 
 int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         uint64_t seed, int32_t variant, int64_t out[10]) {
     if (!out) return ATR_E_INVALID;
-    unsigned long long h[20];
+    unsigned long long h[kCounterSlots];
     const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
     if (rc != ATR_OK) return rc;
     for (int k = 0; k < 10; ++k) out[k] = int64_t(h[k]);
@@ -1399,10 +1408,20 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
 int atr_render_phase_clocks(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                             uint64_t seed, int32_t variant, int64_t out[6]) {
     if (!out) return ATR_E_INVALID;
-    unsigned long long h[20];
+    unsigned long long h[kCounterSlots];
     const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
     if (rc != ATR_OK) return rc;
     for (int k = 0; k < 6; ++k) out[k] = int64_t(h[10 + k]);
+    return ATR_OK;
+}
+
+int atr_render_path_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                             uint64_t seed, int32_t variant, int64_t out[6]) {
+    if (!out) return ATR_E_INVALID;
+    unsigned long long h[kCounterSlots];
+    const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
+    if (rc != ATR_OK) return rc;
+    for (int k = 0; k < 6; ++k) out[k] = int64_t(h[16 + k]);
     return ATR_OK;
 }
 
@@ -1430,8 +1449,7 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost.p);
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);
+    apply_tuning(c, P);
     HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_CLUSTER), nullptr));  // per-cell clocks
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
@@ -1491,8 +1509,7 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
     P.ray_casts = fr->ray_casts;
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);
+    apply_tuning(c, P);
     const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     for (int32_t g = 0; g < ngroups; ++g) {
@@ -1639,7 +1656,7 @@ int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles,
                     st[k++] = owner[size_t(blk.y0 + (lane >> 3)) * size_t(width) + size_t(blk.x0 + (lane & 7))];
         }
         // a hipMemcpy below may overwrite a buffer a kernel on another stream still reads
-        if (bs->used) HIPCHK(hipEventSynchronize(bs->ev));
+        HIPCHK(wait_list(bs->evs));
         const size_t need = st.size() * sizeof(int32_t);
         if (bs->dev_tile.n < need) {
             if (bs->dev_tile.p) (void)hipFree(bs->dev_tile.p);
@@ -1701,8 +1718,7 @@ int atr_render_cell_costs(atr_ctx* c, const atr_camera* cam, uint64_t seed, int3
     P.framebuffer = static_cast<uint32_t*>(fb.p);
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost.p);
-    P.xcd_chunk = xcd_chunk();
-    set_hybrid(P);
+    apply_tuning(c, P);
     if (variant == ATR_KERNEL_PERSIST || variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;  // cell kernels only
     const int sched = auto_sched(variant, *cam);
     HIPCHK(atr_launch_render(P, sched, nullptr));

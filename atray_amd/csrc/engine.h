@@ -175,6 +175,9 @@ struct RenderParams {
     float* hit_t;
     float* rgb;
     uint32_t* ray_casts;
+    // 64 traced-ray counters 128 B apart (a zeroed 8-KB slot of the context's ring, capi.cpp
+    // launch_render); the kernel adds each wave's count to slot (block & 63). Never a caller's
+    // single accumulator: atr_launch_render rejects it together with `counters`.
     unsigned long long* traced_rays;
     int32_t* error_flag;  // set to 1 if a ray hit a traversal limit (never for depth <= 16)
     unsigned long long* counters;  // non-null -> instrumented kernel (10 u64, see render.hip)

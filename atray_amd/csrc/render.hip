@@ -747,6 +747,11 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
         }
         else if constexpr (sched_coop(SCHED)) { if (!__syncthreads_or(go)) break; }
         else if (!go) break;
+        if constexpr (COUNT) {
+            const int bk = i < 2 ? i : 2;
+            ct.steps[bk] += (threadIdx.x & 63) == 0 ? 1u : 0u;
+            ct.active[bk] += go ? 1u : 0u;
+        }
         Isect id;
         id.type = T_NONE;
         if constexpr (STASH) {
@@ -956,6 +961,15 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
             if (lane == 0 && x) atomicAdd(C + 8 + k, (unsigned long long)x);
         }
+        // counters[16..21]: bounce-loop wave steps and tracing lanes, bounce 0 / 1 / >= 2
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            uint32_t a = ct.steps[k], q = ct.active[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) { a += __shfl_xor(a, off); q += __shfl_xor(q, off); }
+            if (lane == 0 && a) atomicAdd(C + 16 + k, (unsigned long long)a);
+            if (lane == 0 && q) atomicAdd(C + 19 + k, (unsigned long long)q);
+        }
         // counters[10..15]: wave clocks in DFS passes, lane-private scans, dealt rounds, whole
         // wave, per-step preparation (leaf range, prefix sums, decision), whole FLAT/HYBRID scan
         if (lane == 0 && in_range) {
@@ -1087,6 +1101,7 @@ static void launch_sched(const atr::RenderParams& P, bool count, bool prim, hipS
 // sched: 0 LANE, 1 WAVE, 2 TILE4, 3 TILE8, 4 CLUSTER; 16 + n: LANE at n waves/SIMD (diagnostic)
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, hipStream_t s) {
     if (P.nblocks <= 0) return hipSuccess;
+    if (P.traced_rays && P.counters) return hipErrorInvalidValue;  // traced_rays is a ring slot (engine.h)
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);

@@ -24,6 +24,9 @@ struct Ctr {
     // wave clocks (s_memtime) in the FLAT/HYBRID scan's phases: DFS passes, lane-private leaf
     // scans, dealt rounds (atr_render_phase_clocks)
     uint32_t t_pass = 0, t_lp = 0, t_deal = 0, t_prep = 0, t_scan = 0;  // per-wave deltas < 2^32
+    // bounce-loop lane use (atr_render_path_counters): wave steps (counted by lane 0) and lanes
+    // tracing in them, for bounce 0, bounce 1 and bounces >= 2
+    uint32_t steps[3] = {0, 0, 0}, active[3] = {0, 0, 0};
 };
 
 struct Ray {

@@ -84,6 +84,12 @@ class atr_frame(C.Structure):
                 ("traced_rays", C.c_void_p)]
 
 
+class atr_tuning(C.Structure):
+    _fields_ = [("xcd_chunk", C.c_int32), ("frame_rotate", C.c_int32), ("hybrid_a", C.c_int32),
+                ("hybrid_b", C.c_int32), ("persist_chunk", C.c_int32), ("cluster_size", C.c_int32),
+                ("reserved", C.c_int32 * 6)]
+
+
 # every symbol include/atray.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = [
     "atr_mesh_load_obj", "atr_mesh_parse_obj", "atr_mesh_from_arrays", "atr_mesh_free",
@@ -97,7 +103,8 @@ EXPORTS = [
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
-    "atr_render_phase_clocks",
+    "atr_render_phase_clocks", "atr_render_path_counters", "atr_default_tuning", "atr_set_tuning",
+    "atr_get_tuning",
 ]
 
 _lib = None
@@ -152,6 +159,10 @@ def lib():
         "atr_packed_tile_ray_casts": ([vp, vp, i32, i32, i32, vp, i32, i64, vp, vp], C.c_int),
         "atr_set_cell_plan": ([vp, i32, i32, vp], C.c_int),
         "atr_render_phase_clocks": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
+        "atr_default_tuning": ([P(atr_tuning)], None),
+        "atr_set_tuning": ([vp, P(atr_tuning)], C.c_int),
+        "atr_get_tuning": ([vp, P(atr_tuning)], C.c_int),
+        "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
         "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
         "atr_render_start_progressive": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32, i32],
@@ -519,6 +530,32 @@ class Engine:
         check(lib().atr_render_phase_clocks(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed),
                                             int(variant), out), "phase clocks")
         return dict(zip(["pass", "lane_private", "dealt", "wave", "step_prep", "scan"], list(out)))
+
+    def tuning(self):
+        """The context's scheduling knobs (atr_get_tuning) as a dict."""
+        t = atr_tuning()
+        check(lib().atr_get_tuning(self.h, C.byref(t)), "get tuning")
+        return {f: getattr(t, f) for f, _ in atr_tuning._fields_ if f != "reserved"}
+
+    def set_tuning(self, **kw):
+        """Change scheduling knobs (atr_set_tuning); unnamed fields keep their current value. Outputs
+        never change; cluster_size applies at the next upload."""
+        t = atr_tuning()
+        check(lib().atr_get_tuning(self.h, C.byref(t)), "get tuning")
+        for k, v in kw.items():
+            if k not in {f for f, _ in atr_tuning._fields_} or k == "reserved":
+                raise KeyError(k)
+            setattr(t, k, int(v))
+        check(lib().atr_set_tuning(self.h, C.byref(t)), "set tuning")
+
+    def path_counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
+        """Bounce-loop lane use (diagnostic): wave steps and tracing lanes of bounce 0, 1, >= 2."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        out = (C.c_int64 * 6)()
+        check(lib().atr_render_path_counters(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed),
+                                             int(variant), out), "path counters")
+        v = list(out)
+        return {"steps": v[:3], "active": v[3:], "lane_use": [a / (64.0 * s) if s else 0.0 for s, a in zip(v[:3], v[3:])]}
 
     def cell_costs(self, cam, seed, variant=ATR_KERNEL_AUTO):
         """Shader clocks per 8x8 cell of one full-frame render ((H+7)/8, (W+7)/8)."""

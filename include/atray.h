@@ -152,6 +152,26 @@ int atr_create(int device, atr_ctx** out);
 int atr_destroy(atr_ctx* ctx);
 const char* atr_version(void);
 
+/* Scheduling knobs of a context. They change launch order and work distribution only, never an
+   output bit (every value is covered by the GPU parity tests). atr_default_tuning fills the
+   measured defaults; atr_set_tuning validates and copies (ATR_E_INVALID on an out
+   of range field or a nonzero reserved word); cluster_size takes effect at the next
+   atr_scene_upload, the others at the next launch. */
+typedef struct {
+    int32_t xcd_chunk;      /* cell schedules: consecutive workgroups per XCD chunk (0 = one
+                               contiguous range per XCD), 0..4096; default 16 */
+    int32_t frame_rotate;   /* multi-frame launches: frame f's cell list starts f/F x this/1024 of
+                               the way in, 0..1024; default 0 */
+    int32_t hybrid_a, hybrid_b; /* HYBRID: a leaf step is dealt over the lanes when the largest
+                               cluster count exceeds a x rounds + b, -4096..4096; default 2, 1 */
+    int32_t persist_chunk;  /* PERSIST: 8x8 cells per work-queue claim, 1..4096; default 16 */
+    int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
+    int32_t reserved[6];    /* must be 0 */
+} atr_tuning;
+void atr_default_tuning(atr_tuning* out);
+int atr_set_tuning(atr_ctx* ctx, const atr_tuning* tuning);
+int atr_get_tuning(atr_ctx* ctx, atr_tuning* out);
+
 /* Flatten + upload the scene (copies; the caller keeps its buffers). prep_scene's tree build
    happens before this call (atr_octree_build); upload is not part of the render timing. */
 int atr_scene_upload(atr_ctx* ctx, const atr_material* materials, int32_t nmaterials,
@@ -240,6 +260,12 @@ int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
    (make EXTRA=-DATR_PHASE_CLOCKS); the product library reports the whole-wave clocks alone. */
 int atr_render_phase_clocks(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                             uint64_t seed, int32_t variant, int64_t out[6]);
+/* Diagnostic: one instrumented render; lane use of the bounce loop (cast_ray, renderer.cpp:213-262)
+   in the wavefront schedules (WAVE, FLAT, HYBRID): out[0..2] = wave steps of bounce 0, 1 and >= 2
+   (a step = one loop iteration some lane of the wave traces in), out[3..5] = lanes tracing in
+   them. out[3 + k] / (64 out[k]) is the lane utilisation of bounce bucket k. */
+int atr_render_path_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                             uint64_t seed, int32_t variant, int64_t out[6]);
 /* Diagnostic: one render of `tiles` recording, per 8x8 work block (block order), the wave's start
    and end on the 100 MHz device clock and its HW_ID | XCC_ID << 32. out = 3 u64 per block;
    with out == NULL (or cap too small) only *nblocks is set. */

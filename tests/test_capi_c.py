@@ -28,7 +28,7 @@ def run(*args):
 def test_struct_layouts_match_ctypes_mirrors():
     lay = run("layout")
     for name in ["atr_vec3", "atr_material", "atr_model", "atr_sphere", "atr_plane", "atr_camera", "atr_tile",
-                 "atr_frame"]:
+                 "atr_frame", "atr_tuning"]:
         cls = getattr(E, name)
         assert lay[f"sizeof({name})"] == C.sizeof(cls), name
         for field, _ in cls._fields_:

@@ -1,5 +1,5 @@
-"""Driver for rocprofv3 --pmc passes (tools/gpu_pmc2.sh): three one-frame c3 renders with the
-given variant, then three atr_unpack launches over the full frame (4-B stores per lane, exactly
+"""Driver for rocprofv3 --pmc passes (tools/gpu_pmc2.sh): three one-frame renders (c3 geometry;
+PMC_SPP / PMC_BOUNCES select e.g. the c4 shape) with the given variant, then three atr_unpack launches over the full frame (4-B stores per lane, exactly
 W*H*4 bytes written and read: the calibration kernel for WRITE_SIZE / FETCH_SIZE)."""
 import os
 import sys
@@ -17,7 +17,7 @@ box = mesh.translate_to(mesh.aabb(), CENTERS["Dragon"])
 tree = E.Octree.build(mesh, 300)
 eng = E.Engine(0)
 eng.upload([((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)], [(mesh, tree, box, 1)])
-cam = E.camera(W, H)
+cam = E.camera(W, H, int(os.environ.get("PMC_SPP", "1")), int(os.environ.get("PMC_BOUNCES", "1")))
 tiles = [[0, 0, W - 1, H - 1]]
 fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
 casts = torch.zeros(W * H, dtype=torch.int32, device="cuda")
