@@ -1389,7 +1389,9 @@ static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.counters = static_cast<unsigned long long*>(ctr.p);
     apply_tuning(c, P);  // the product's HYBRID thresholds (the counts do not depend on them, the clocks do)
     const int sc = auto_sched(variant, *cam);
-    HIPCHK(launch_render(c, P, sc >= 32 ? 4 : (sc >= 16 ? 0 : sc), nullptr));
+    // diagnostic codes: the CC schedules (96+) have COUNT builds; other occupancy variants count
+    // with their base schedule
+    HIPCHK(launch_render(c, P, sc >= 96 ? sc : (sc >= 32 ? 4 : (sc >= 16 ? 0 : sc)), nullptr));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h, ctr.p, kCounterSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;
@@ -1422,6 +1424,19 @@ int atr_render_path_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* 
     const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
     if (rc != ATR_OK) return rc;
     for (int k = 0; k < 6; ++k) out[k] = int64_t(h[16 + k]);
+    return ATR_OK;
+}
+
+int atr_render_simd_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                             uint64_t seed, int32_t variant, int64_t out[7]) {
+    if (!out) return ATR_E_INVALID;
+    unsigned long long h[kCounterSlots];
+    const int rc = count_launch(c, cam, tiles, ntiles, seed, variant, h);
+    if (rc != ATR_OK) return rc;
+    out[0] = int64_t(h[22]);  // candidate-loop wave iterations
+    out[1] = int64_t(h[2]);   // full triangle tests (lane level)
+    for (int k = 0; k < 4; ++k) out[2 + k] = int64_t(h[23 + k]);
+    out[6] = int64_t(h[0]);   // traced rays
     return ATR_OK;
 }
 

@@ -59,10 +59,21 @@ __device__ __forceinline__ void cluster_tri_test(const Ray& r, float4_t q0, floa
     }
 }
 
+// The full-test operands of slot k: a, ab, ac and the leaf rank (c2.y). (64-B slot records, one
+// cache line per test, measured no faster once the candidates are compacted: DESIGN.md §4f.)
+__device__ __forceinline__ void load_prim(const DModel& m, uint32_t k, float4_t& a0, float4_t& a1, c2_t& a2) {
+    a0 = m.c0[k];
+    a1 = m.c1[k];
+    a2 = m.c2[k];
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, LeafHit& h,
                                             Ctr& ct) {
-    cluster_tri_test<COUNT>(r, m.c0[k], m.c1[k], m.c2[k], k, h, ct);
+    float4_t a0, a1;
+    c2_t a2;
+    load_prim(m, k, a0, a1, a2);
+    cluster_tri_test<COUNT>(r, a0, a1, a2, k, h, ct);
 }
 
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
@@ -140,11 +151,11 @@ __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float
     return gc;
 }
 
-// Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and
-// the full tests of its primitives.
-template <bool COUNT, bool PAIR = false>
-__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
-                                             LeafHit& h, Ctr& ct) {
+// Cluster c of a leaf: the padded box tests and the screen against the bound `best`. Returns the
+// mask of the primitives (slot 16 c + bit) that still need the full test.
+template <bool COUNT>
+__device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
+                                                  float best, Ctr& ct) {
     // the screen constants (7 values) are recomputed for every cluster from an opaque copy of the
     // ray instead of being hoisted out of the scan loops and held through the passes and rounds:
     // ~10 VALU per cluster for 7 VGPRs, what lets HYBRID run 6 waves/SIMD
@@ -152,8 +163,7 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     asm volatile("" : "+v"(rr.d.x), "+v"(rr.d.y), "+v"(rr.d.z), "+v"(rr.inv.x), "+v"(rr.inv.y), "+v"(rr.inv.z));
     const ScreenRay sr = screen_ray(rr);
     float dlo, dhi;
-    if (!cluster_pads(r, sr, lo, hi, h.t, dlo, dhi)) return;
-    const uint32_t first = kMaxClusterSize * c;
+    if (!cluster_pads(r, sr, lo, hi, best, dlo, dhi)) return 0;
     const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u;
     if constexpr (COUNT) ct.screen += n;
     const uint4_t* nb = m.cnrm + kClusterBlock * size_t(c);
@@ -161,25 +171,39 @@ __device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
         cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8], g, n) << g;
+    return cand;
+}
+
+// Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and
+// the full tests of its primitives.
+template <bool COUNT, bool PAIR = false>
+__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
+                                             LeafHit& h, Ctr& ct) {
+    uint32_t cand = cluster_cands<COUNT>(r, m, c, lo, hi, h.t, ct);
+    const uint32_t first = kMaxClusterSize * c;
     if constexpr (!PAIR) {
         // one at a time: the lane-private CLUSTER kernel's peak stays at 94 VGPRs (no scratch at
         // 5 waves/SIMD); two in flight measured slower there
         while (cand) {
+            if constexpr (COUNT) ct.cand_wave += first_active_lane();
             const uint32_t k = first + uint32_t(__builtin_ctz(cand));
             cand &= cand - 1;
-            cluster_tri_test<COUNT>(r, m.c0[k], m.c1[k], m.c2[k], k, h, ct);
+            cluster_tri<COUNT>(r, m, k, h, ct);
         }
     } else {
         while (cand) {  // two primitives' loads in flight (FLAT: faster despite the registers)
+            if constexpr (COUNT) ct.cand_wave += first_active_lane();
             const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
             cand &= cand - 1;
-            const float4_t a0 = m.c0[ka], a1 = m.c1[ka];
-            const c2_t a2 = m.c2[ka];
+            float4_t a0, a1;
+            c2_t a2;
+            load_prim(m, ka, a0, a1, a2);
             if (cand) {
                 const uint32_t kb = first + uint32_t(__builtin_ctz(cand));
                 cand &= cand - 1;
-                const float4_t b0 = m.c0[kb], b1 = m.c1[kb];
-                const c2_t b2 = m.c2[kb];
+                float4_t b0, b1;
+                c2_t b2;
+                load_prim(m, kb, b0, b1, b2);
                 cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
                 cluster_tri_test<COUNT>(r, b0, b1, b2, kb, h, ct);
             } else {

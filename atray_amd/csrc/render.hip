@@ -300,6 +300,19 @@ __device__ __forceinline__ FlatLds& flat_lds() {
     return L;
 }
 
+// Full tests of a round's candidates, compacted over the wavefront (CC). Each lane holds one
+// (ray, cluster) item that passed the padded boxes and the screen with candidate mask `cm`
+// (slots cfirst + bit, ray of lane `own`); the wave's candidates are numbered by a prefix sum of
+// the masks' popcounts and dealt 64 per sub-round, one full test per lane: a cluster's
+// candidates no longer run one after another in one lane (the serial chain of dependent loads
+// that set the slow cells' time) while the other lanes wait. Each test lowers its owner's
+// (t bits, leaf rank) key in LDS -- the minimum over the leaf in any order is the reference's
+// first-in-leaf-order closest hit (kd_tree.cpp:440-456) -- and the winning test writes the slot
+// and barycentrics.
+template <bool COUNT, bool UO, bool NUV>
+__device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
+                                            uint32_t cfirst, int32_t own, Ctr& ct);
+
 // HYB (the HYBRID schedule): each step the wavefront decides, uniformly, how to scan its rays'
 // current leaves: lane-private (every lane scans its own leaf's clusters, as CLUSTER does: no
 // per-round overhead, best when the rays' cluster counts are alike) or dealt in rounds (FLAT:
@@ -308,8 +321,70 @@ __device__ __forceinline__ FlatLds& flat_lds() {
 // hyb_a / hyb_b). A leaf's result does not depend on how its clusters were visited (minimum
 // (t, leaf rank)), so the choice changes no output bit. LDSB: the DFS pass inserts straight
 // into the LDS columns (CLUSTER's LdsLeafBuf) instead of a register buffer copied after it.
+template <bool COUNT, bool UO, bool NUV>
+__device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
+                                            uint32_t cfirst, int32_t own, Ctr& ct) {
+    constexpr unsigned long long kInit = (static_cast<unsigned long long>(0x7F7FFFFFu) << 32) | 0xFFFFFFFFull;
+    FlatLds& L = flat_lds();
+    const uint32_t cc = uint32_t(__popc(cm));
+    const uint32_t cinc = wave_incl_add(cc);
+    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(cinc), 63));
+    const uint32_t cex = cinc - cc;
+    int32_t carry = -1;
+    for (uint32_t cb = 0; cb < total; cb += 64) {  // wave-uniform
+        L.mark[w][ln] = -1;
+        __builtin_amdgcn_wave_barrier();
+        if (cc > 0 && cex >= cb && cex < cb + 64u) L.mark[w][cex - cb] = ln;
+        __builtin_amdgcn_wave_barrier();
+        int32_t src = wave_incl_max(L.mark[w][ln]);  // the lane whose candidates hold number cb + ln
+        if (src < 0) src = carry;
+        carry = __builtin_amdgcn_readlane(src, 63);
+        const uint32_t k = cb + uint32_t(ln);
+        const bool valid = k < total;
+        const int32_t s2 = valid ? src : ln;
+        uint32_t j = k - uint32_t(__shfl(int(cex), s2));
+        uint32_t x = uint32_t(__shfl(int(cm), s2));
+        uint32_t b = 0, n;  // position of the j-th set bit of the 16-bit mask x
+        n = uint32_t(__popc(x & 0xFFu)); if (j >= n) { j -= n; x >>= 8; b += 8; }
+        n = uint32_t(__popc(x & 0xFu)); if (j >= n) { j -= n; x >>= 4; b += 4; }
+        n = uint32_t(__popc(x & 0x3u)); if (j >= n) { j -= n; x >>= 2; b += 2; }
+        b += j >= (x & 1u) ? 1u : 0u;
+        const uint32_t slot = uint32_t(__shfl(int(cfirst), s2)) + b;
+        const int32_t ow = __shfl(own, s2);
+        Ray q;
+        q.o = UO ? r.o : mk(shfl_f(r.o.x, ow), shfl_f(r.o.y, ow), shfl_f(r.o.z, ow));
+        q.d = mk(shfl_f(r.d.x, ow), shfl_f(r.d.y, ow), shfl_f(r.d.z, ow));
+        unsigned long long mine = kInit;
+        bool imp = false;
+        float u = 0.f, v = 0.f;
+        if (valid) {
+            if constexpr (COUNT) { ct.tri += 1; ct.cand_wave += ln == 0 ? 1u : 0u; }
+            float4_t a0, a1;
+            c2_t a2;
+            load_prim(m, slot, a0, a1, a2);
+            const float dist = tri_hit(q, mk(a0.x, a0.y, a0.z), mk(a0.w, a1.x, a1.y), mk(a1.z, a1.w, a2.x), u, v);
+            if (dist > kTol && dist < kMaxFloat) {  // accepted (model.h:75-103; kd_tree.cpp:450)
+                mine = (static_cast<unsigned long long>(__float_as_uint(dist)) << 32) | uint32_t(__float_as_int(a2.y));
+                if (mine < L.key[w][ow]) {
+                    atomicMin(&L.key[w][ow], mine);
+                    imp = true;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (imp && L.key[w][ow] == mine) {  // this sub-round's winner for its owner
+            L.slot[w][ow] = slot;
+            if constexpr (!NUV) {
+                L.u[w][ow] = u;
+                L.v[w][ow] = v;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false, bool UT = false,
-          bool NUV = false>
+          bool NUV = false, bool CC = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
@@ -405,7 +480,20 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         bool lp_imp = false;  // lane-private scan: this lane's leaf improved its hit
         ATR_PCLK(const uint64_t tc1 = clock64());
         ATR_PCLK(ct.t_prep += uint32_t(tc1 - tc2));
-        if (!deal) {
+        if (!deal && CC) {  // every lane scans its own leaf's clusters, one per iteration; the
+                            // candidates of each iteration are compacted over the wave
+            const uint32_t mxc = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
+            for (uint32_t i = 0; i < mxc; ++i) {
+                uint32_t cm = 0;
+                if (i < cn) {
+                    const uint32_t c = cf + i;
+                    const float bound = __uint_as_float(uint32_t(s_key[w][ln] >> 32));
+                    cm = cluster_cands<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)],
+                                              m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
+                }
+                cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
+            }
+        } else if (!deal) {
             if (cn > 0) {
                 LeafHit lh;
                 lh.t = kMaxFloat;
@@ -435,6 +523,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             carry = __builtin_amdgcn_readlane(own, 63);
             const uint32_t k = base + uint32_t(ln);
             const bool valid = k < total;
+            if constexpr (COUNT) { ct.round_wave += ln == 0 ? 1u : 0u; ct.round_items += valid ? 1u : 0u; }
             const int32_t src = valid ? own : ln;
             Ray q;  // the owner's ray
             // UO: every ray of the wave starts at the same point (primary rays: the frame's eye)
@@ -445,6 +534,16 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             q.s1 = q.inv.y < 0;
             q.s2 = q.inv.z < 0;
             const uint32_t c = uint32_t(__shfl(int(cf), src)) + (k - uint32_t(__shfl(int(excl), src)));
+            if constexpr (CC) {
+                uint32_t cm = 0;
+                if (valid) {
+                    const float bound = __uint_as_float(uint32_t(s_key[w][own] >> 32));
+                    cm = cluster_cands<COUNT>(q, m, c, m.clus[kClusterBlock * size_t(c)],
+                                              m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
+                }
+                cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
+                continue;
+            }
             unsigned long long mine = kInit;
             LeafHit lh;
             lh.improved = false;
@@ -476,7 +575,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
         if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
             bool imp = lp_imp;
-            if (deal) {
+            if (deal || CC) {
                 const unsigned long long key = s_key[w][ln];
                 imp = key != kInit;
                 if (imp) {
@@ -657,11 +756,17 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 
 // ------------------------------------------------------------------ get_intersection_data
 enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5,
-       SCHED_FLAT = 6, SCHED_HYBRID = 7 };
+       SCHED_FLAT = 6, SCHED_HYBRID = 7, SCHED_FLAT_NOCC = 9, SCHED_HYBRID_NOCC = 10, SCHED_FLAT_UT = 11 };
+// The FLAT / HYBRID family (wave-wide leaf steps, LDS path stash). FLAT and HYBRID compact the full
+// tests' candidates over the wavefront (cand_rounds); the _NOCC schedules are the round-2 kernels
+// that test a cluster's candidates in its lane (diagnostic); FLAT_UT walks every
+// bounce's DFS passes wave-wide (diagnostic).
+constexpr bool sched_flat(int sc) { return sc == SCHED_FLAT || sc == SCHED_FLAT_NOCC || sc == SCHED_FLAT_UT; }
+constexpr bool sched_hyb(int sc) { return sc == SCHED_HYBRID || sc == SCHED_HYBRID_NOCC; }
+constexpr bool sched_cc(int sc) { return sc != SCHED_FLAT_NOCC && sc != SCHED_HYBRID_NOCC; }
 constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
 constexpr bool sched_coop(int sc) {  // lanes must stay in lockstep loops (workgroup-wide)
-    return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && sc != SCHED_FLAT &&
-           sc != SCHED_HYBRID;
+    return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && !sched_flat(sc) && !sched_hyb(sc);
 }
 
 template <int SCHED, bool COUNT, bool PR = false>
@@ -679,15 +784,19 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
             Hit h;
             if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
-            else if constexpr (SCHED == SCHED_FLAT) {
+            else if constexpr (sched_flat(SCHED)) {
+                constexpr bool CC = sched_cc(SCHED);
                 // the camera rays of a bounce loop (one origin, coherent) take HYBRID's primary flavour
-                if (first) tree_closest_flat<COUNT, true, true, false, true, true>(r, m, active, h, err, ct, hyb_a, hyb_b);
-                else tree_closest_flat<COUNT>(r, m, active, h, err, ct);
+                if (first)
+                    tree_closest_flat<COUNT, true, true, false, true, true, false, CC>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                else if constexpr (SCHED == SCHED_FLAT_UT)
+                    tree_closest_flat<COUNT, false, true, true, false, true, false, CC>(r, m, active, h, err, ct);
+                else tree_closest_flat<COUNT, false, false, true, false, false, false, CC>(r, m, active, h, err, ct);
             }
-            else if constexpr (SCHED == SCHED_HYBRID)
+            else if constexpr (sched_hyb(SCHED))
                 // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
                 // bounces: FLAT's register buffer and paired candidate loads (measured)
-                tree_closest_flat<COUNT, true, PR, !PR, PR, PR, PR>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                tree_closest_flat<COUNT, true, PR, !PR, PR, PR, PR, sched_cc(SCHED)>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {
@@ -732,7 +841,7 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
                                        bool active, uint64_t& st, uint64_t stream, uint32_t& casts,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
                                        int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b, V3& acc) {
-    constexpr bool STASH = SCHED == SCHED_FLAT || SCHED == SCHED_HYBRID;
+    constexpr bool STASH = sched_flat(SCHED) || sched_hyb(SCHED);
     __shared__ uint32_t s_stash[STASH ? 4 : 1][kStash][64];
     uint32_t* L = &s_stash[STASH ? threadIdx.x >> 6 : 0][0][threadIdx.x & 63];
     V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
@@ -742,7 +851,7 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
     // cooperate on leaf scans inside intersect_scene.
     for (i = 0; ; ++i) {
         const bool go = live && i < bounce_limit;
-        if constexpr (SCHED == SCHED_WAVE || SCHED == SCHED_FLAT || SCHED == SCHED_HYBRID) {
+        if constexpr (SCHED == SCHED_WAVE || sched_flat(SCHED) || sched_hyb(SCHED)) {
             if (__ballot(go) == 0) break;
         }
         else if constexpr (sched_coop(SCHED)) { if (!__syncthreads_or(go)) break; }
@@ -970,6 +1079,18 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
             if (lane == 0 && a) atomicAdd(C + 16 + k, (unsigned long long)a);
             if (lane == 0 && q) atomicAdd(C + 19 + k, (unsigned long long)q);
         }
+        // counters[22..26]: SIMD efficiency (candidate-loop wave iterations, DFS wave / lane
+        // iterations, dealt rounds, dealt items)
+        {
+            uint32_t e[5] = {ct.cand_wave, ct.node_wave, ct.node_lane, ct.round_wave, ct.round_items};
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                uint32_t x = e[k];
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+                if (lane == 0 && x) atomicAdd(C + 22 + k, (unsigned long long)x);
+            }
+        }
         // counters[10..15]: wave clocks in DFS passes, lane-private scans, dealt rounds, whole
         // wave, per-step preparation (leaf range, prefix sums, decision), whole FLAT/HYBRID scan
         if (lane == 0 && in_range) {
@@ -987,6 +1108,11 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
 #define ATR_INST4(SC) ATR_INST(SC, false, false) ATR_INST(SC, true, false) ATR_INST(SC, false, true) ATR_INST(SC, true, true)
 ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCHED_TILE8) ATR_INST4(SCHED_CLUSTER)
 ATR_INST4(SCHED_FLAT) ATR_INST4(SCHED_HYBRID)
+ATR_INST(SCHED_FLAT_NOCC, false, false) ATR_INST(SCHED_FLAT_NOCC, true, false)
+ATR_INST(SCHED_FLAT_UT, false, false) ATR_INST(SCHED_FLAT_UT, true, false)
+ATR_INST(SCHED_HYBRID_NOCC, true, true) ATR_INST(SCHED_HYBRID_NOCC, true, false)
+ATR_INST(SCHED_HYBRID_NOCC, false, false)
+template __global__ void render_kernel<SCHED_HYBRID_NOCC, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 7>(RenderParams);
@@ -1105,6 +1231,25 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);
+    if (sched >= 96) {  // diagnostic: 96 FLAT and 97 HYBRID without candidate compaction (round 2),
+                        // 100 FLAT with wave-walked DFS passes on every bounce
+        if (sched == 96) {
+            if (prim) return hipErrorInvalidValue;
+            if (count) launch_one<atr::SCHED_FLAT_NOCC, true, false>(P, s);
+            else launch_one<atr::SCHED_FLAT_NOCC, false, false>(P, s);
+        } else if (sched == 97) {
+            if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID_NOCC, false, true, 6>), g, b, 0, s, P);
+            else if (count) { if (prim) launch_one<atr::SCHED_HYBRID_NOCC, true, true>(P, s); else launch_one<atr::SCHED_HYBRID_NOCC, true, false>(P, s); }
+            else launch_one<atr::SCHED_HYBRID_NOCC, false, false>(P, s);
+        } else if (sched == 100) {
+            if (prim) return hipErrorInvalidValue;
+            if (count) launch_one<atr::SCHED_FLAT_UT, true, false>(P, s);
+            else launch_one<atr::SCHED_FLAT_UT, false, false>(P, s);
+        } else {
+            return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (sched >= 80) {  // HYBRID at 80 + n waves/SIMD (diagnostic)
         const int o = sched - 80;
         if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 5>), g, b, 0, s, P);

@@ -27,7 +27,15 @@ struct Ctr {
     // bounce-loop lane use (atr_render_path_counters): wave steps (counted by lane 0) and lanes
     // tracing in them, for bounce 0, bounce 1 and bounces >= 2
     uint32_t steps[3] = {0, 0, 0}, active[3] = {0, 0, 0};
+    // SIMD efficiency (atr_render_simd_counters): wave-level iterations of the full-test candidate
+    // loops, DFS loop iterations at wave and lane level, dealt rounds and the items they carried
+    uint32_t cand_wave = 0, node_wave = 0, node_lane = 0, round_wave = 0, round_items = 0;
 };
+
+// 1 in the lowest active lane of the wavefront (counts a divergent loop's wave-level iterations)
+__device__ __forceinline__ uint32_t first_active_lane() {
+    return (threadIdx.x & 63) == uint32_t(__builtin_ctzll(__ballot(1))) ? 1u : 0u;
+}
 
 struct Ray {
     V3 o, d, inv;
@@ -356,6 +364,7 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
     uint32_t bm = cur.bm;
     int32_t parent = -1, lvl = 0;
     for (;;) {
+        if constexpr (COUNT) { ct.node_wave += first_active_lane(); ct.node_lane += 1; }
         const uint32_t m = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
         if (m) {
             const int s = 31 - __clz(m);
@@ -402,6 +411,7 @@ __device__ __forceinline__ int32_t traverse_pass_wave(const Ray& r, const float4
     uint32_t bm = cur.bm;  // wave-uniform walk state
     int32_t parent = -1, lvl = 0;
     for (;;) {
+        if constexpr (COUNT) { ct.node_wave += (threadIdx.x & 63) == 0 ? 1u : 0u; ct.node_lane += part ? 1u : 0u; }
         const uint32_t mine = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
         int s = -1;  // highest child any lane still has to visit at this level
         for (int b = 7; b >= 0; --b)

@@ -104,7 +104,7 @@ EXPORTS = [
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_render_phase_clocks", "atr_render_path_counters", "atr_default_tuning", "atr_set_tuning",
-    "atr_get_tuning",
+    "atr_get_tuning", "atr_render_simd_counters",
 ]
 
 _lib = None
@@ -162,6 +162,7 @@ def lib():
         "atr_default_tuning": ([P(atr_tuning)], None),
         "atr_set_tuning": ([vp, P(atr_tuning)], C.c_int),
         "atr_get_tuning": ([vp, P(atr_tuning)], C.c_int),
+        "atr_render_simd_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
         "atr_render_wait": ([vp, u32, P(i32)], C.c_int),
@@ -556,6 +557,16 @@ class Engine:
                                              int(variant), out), "path counters")
         v = list(out)
         return {"steps": v[:3], "active": v[3:], "lane_use": [a / (64.0 * s) if s else 0.0 for s, a in zip(v[:3], v[3:])]}
+
+    def simd_counters(self, cam, tiles, seed, variant=ATR_KERNEL_AUTO):
+        """SIMD efficiency of the clustered scans (diagnostic, atr_render_simd_counters)."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        out = (C.c_int64 * 7)()
+        check(lib().atr_render_simd_counters(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed),
+                                             int(variant), out), "simd counters")
+        keys = ["cand_wave_iters", "full_tests", "dfs_wave_iters", "dfs_lane_iters", "dealt_rounds", "dealt_items",
+                "rays"]
+        return dict(zip(keys, [int(x) for x in out]))
 
     def cell_costs(self, cam, seed, variant=ATR_KERNEL_AUTO):
         """Shader clocks per 8x8 cell of one full-frame render ((H+7)/8, (W+7)/8)."""

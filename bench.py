@@ -98,23 +98,36 @@ def cpu_share():
     return max(1, n)
 
 
-def pmc_traffic(args, kernel_name, frames):
-    """HBM bytes per render launch of `frames` frames (the timed launches' shape) from two
-    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a short child run of this benchmark that
-    renders one such launch; the rows of the largest render grid are that launch. FETCH_SIZE is
-    doubled (MI355X_MICROARCH.md, HBM: gfx950 reports half the bytes of wide reads); both counters
-    are in KB."""
+# PMC passes of the child run, one counter group per rocprofv3 run (gfx950 block limits: FETCH_SIZE
+# takes 3 of the 4 TCC counters, WRITE_SIZE 2, so each gets its own pass).
+PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"],
+              ["SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"],
+              ["TCC_HIT_sum", "TCC_MISS_sum"]]
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2.0  # wave-instructions/s: 1,024 SIMD-32s, one wave64 VALU op per 2 clocks
+                                          # (MI355X_MICROARCH.md "Wave scheduling"), 2.4 GHz
+
+
+def pmc_counters(args, kernel_name):
+    """Counters of the timed launches of THIS command's shape: a child run of bench.py with the same
+    --config/--steps/--warmup/--streams/--frames-per-launch/--variant (no PMC, no CPU baseline),
+    profiled by separate rocprofv3 --pmc passes. Per counter: the mean over the launches of the
+    largest render grid (the timed launches; warmup and priming launches are smaller or equal in
+    shape and are excluded when smaller). Returns ({counter: mean per launch}, frames per such
+    launch, note)."""
     exe = "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
-        return None, "rocprofv3 missing"
+        return None, 0, "rocprofv3 missing"
     out = {}
-    for ctr in ["FETCH_SIZE", "WRITE_SIZE"]:
-        d = os.path.join(ROOT, "gpurun_out", f"pmc_{ctr.lower()}")
+    grid = None
+    base = os.path.join(ROOT, "gpurun_out", "bench_pmc")
+    for i, group in enumerate(PMC_PASSES):
+        d = os.path.join(base, f"pass{i}")
         os.makedirs(d, exist_ok=True)
-        cmd = [exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
-               "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(frames), "--warmup", "1",
-               "--frames-per-launch", str(frames), "--streams", "1", "--config", args.config, "--variant", args.variant,
-               "--no-cpu-baseline", "--no-pmc", "--no-prep"]
+        cmd = [exe, "--pmc", *group, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
+               "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup",
+               str(args.warmup), "--frames-per-launch", str(args.frames_per_launch), "--streams", str(args.streams),
+               "--config", args.config, "--variant", args.variant, "--no-cpu-baseline", "--no-pmc", "--no-prep",
+               "--no-steady"]
         env = dict(os.environ)
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
             env.pop(k, None)
@@ -122,22 +135,25 @@ def pmc_traffic(args, kernel_name, frames):
             subprocess.run(cmd, check=True, timeout=300, env=env, stdout=subprocess.DEVNULL,
                            stderr=subprocess.DEVNULL)
         except Exception as e:  # noqa: BLE001
-            return None, f"rocprofv3 {ctr} failed: {e}"
+            return None, 0, f"rocprofv3 {group} failed: {e}"
         rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
                     # product launches only (not the instrumented COUNT build: <.., true, ..>)
-                    if kernel_name in name and not re.search(kernel_name + r"<(\d+, )?true", name) \
-                            and row.get("Counter_Name") == ctr:
-                        rows.append((int(row.get("Grid_Size") or 0), float(row["Counter_Value"])))
+                    if kernel_name in name and not re.search(kernel_name + r"<(\d+, )?true", name):
+                        rows.append((int(row.get("Grid_Size") or 0), row.get("Dispatch_Id"), row["Counter_Name"],
+                                     float(row["Counter_Value"])))
         if not rows:
-            return None, f"no {ctr} rows"
-        big = max(g for g, _ in rows)  # the `frames`-frame launch
-        vals = [v for g, v in rows if g == big]
-        out[ctr] = sum(vals) / len(vals)
-    return 2.0 * out["FETCH_SIZE"] * 1024.0 + out["WRITE_SIZE"] * 1024.0, "ok"
+            return None, 0, f"no rows for {group}"
+        big = max(g for g, _, _, _ in rows)
+        grid = big if grid is None else grid
+        for c in group:
+            vals = [v for g, _, n, v in rows if g == big and n == c]
+            if vals:
+                out[c] = sum(vals) / len(vals)
+    return out, grid, "ok"
 
 
 def cpu_baseline(asset, W, H, spp, bounces, use_tree, seconds):
@@ -212,6 +228,13 @@ def launch_sizes(k, f, s=1):
 VARIANT_NAMES = {}
 
 
+def calib_frames(args):
+    """Orbit positions the cost plan is calibrated on: the last calib_frames positions before the
+    timed window (warmup - c, ..., warmup - 1, taken modulo the orbit), never a timed frame."""
+    c = max(1, args.calib_frames)
+    return sorted({(args.warmup - c + i) % ORBIT_PERIOD for i in range(c)})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,11 +244,16 @@ def main():
     ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps", "flat", "hyb"])
     ap.add_argument("--variant-code", type=int, default=-1,
                     help="diagnostic: raw kernel code passed to the engine (overrides --variant's kernel)")
+    ap.add_argument("--tuning", default="",
+                    help="diagnostic: k=v,... scheduling knobs for atr_set_tuning (xcd_chunk, frame_rotate, hybrid_a, "
+                         "hybrid_b, persist_chunk, cluster_size); outputs never change")
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-prep", action="store_true", help="skip the device octree build timing")
+    ap.add_argument("--no-steady", action="store_true",
+                    help="skip the steady-state figure (64 further frames in 16-frame launches, after the timed region)")
     ap.add_argument("--no-orbit", action="store_true", help="every frame from the app camera")
     ap.add_argument("--streams", type=int, default=2, help="launches in flight (one HIP stream each)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
@@ -384,6 +412,8 @@ def run(args):
         tree = E.Octree.build(mesh, 300)
         prep["octree_host_ms"] = round((time.perf_counter() - t) * 1e3, 2)
     eng = E.Engine(local % ndev)
+    if args.tuning:
+        eng.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in args.tuning.split(","))})
     if use_tree and not args.no_prep and rank == 0:
         tm = {}
         E.Octree.build_device(mesh, 300, local % ndev, timings=tm)  # f3: same tree on the GPU
@@ -405,8 +435,9 @@ def run(args):
     pw, pr = (args.sim_world, args.sim_rank) if sim else (world, rank)  # the plan's world and rank
     heavy_first = args.tile_order == "cost"
     if (pw > 1 and args.plan == "cost") or (pw == 1 and args.single_tiles == "cost"):
-        # measured on a few of the run's own frames (a live renderer would use its previous frames)
-        ks = sorted({args.warmup + (args.steps * i) // max(1, args.calib_frames) for i in range(args.calib_frames)})
+        # measured on frames BEFORE the timed window (the warmup's orbit positions, or the positions
+        # just before them): a live renderer only has its previous frames
+        ks = calib_frames(args)
         costs = np.zeros(len(E.shard_grid(W, H, args.side)), np.int64)
         if rank == 0:
             for k in ks:
@@ -420,7 +451,7 @@ def run(args):
     cell_split = None
     if args.cell_split:  # the heaviest cells of the run's calibration frames, split over P waves
         parts, frac = args.cell_split.split(":")
-        ks = sorted({args.warmup + (args.steps * i) // max(1, args.calib_frames) for i in range(args.calib_frames)})
+        ks = calib_frames(args)
         cc = sum(eng.cell_costs(cams[k % n_orbit], SEED, variant) for k in ks)
         nsplit = int(round(float(frac) * cc.size))
         cplan = np.zeros(cc.size, np.uint8)
@@ -644,6 +675,28 @@ def run(args):
         assert rc == 0
         return float(np.mean([a.elapsed_time(b) for a, b in evs]))
     kern_ms = time_one(roof_variant)
+    # steady state (informational, not `value`): 64 further orbit frames in 16-frame launches on the
+    # same streams, after the timed region -- the rate without a short run's pipeline fill and drain
+    steady = None
+    if not args.no_steady and pw == 1 and world == 1:
+        F0 = F_
+        nst = 64
+        torch.cuda.synchronize()
+        for t_ in traced:
+            t_.zero_()
+        fst = min(16, F0)
+        t1 = time.perf_counter()
+        k0 = args.warmup + args.steps
+        for j, nf in enumerate(launch_sizes(nst, fst, S_)):
+            q = j % S_
+            fr = [cams[(k0 + f) % n_orbit] for f in range(nf)]
+            eng.render_start_cameras(fr, tiles, frame_of(q), own, SEED, stream=streams[q].cuda_stream, variant=variant)
+            k0 += nf
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t1
+        st_rays = int(torch.stack(traced).sum().item())
+        steady = {"frames": nst, "frames_per_launch": fst, "ms_per_frame": round(dt / nst * 1e3, 4),
+                  "mrays_s": round(st_rays / dt / 1e6, 1)}
     live_ctr = eng.counters(app_cam, tiles, SEED, roof_variant) if rank == 0 else None
 
     if rank == 0:
@@ -658,6 +711,7 @@ def run(args):
                                       f"{'octree' if use_tree else 'brute-force'}",
                           "rays_per_step": round(rays_total / args.steps), "shard_tile": args.side,
                           "parallelism": f"tiles{world}", "kernel": args.variant,
+                          **({"tuning": eng.tuning()} if args.tuning else {}),
                           "plan": (f"{args.plan}/{args.tile_order}" if pw > 1 else
                                    "single" if args.single_tiles == "frame" else f"single/{args.tile_order}"),
                           "streams": args.streams, "frames_per_launch": F_,
@@ -667,44 +721,78 @@ def run(args):
                           "shard_pixels": [int(x) for x in sizes]},
                **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange"}} if sim else {}),
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
+        if steady:
+            out["steady_state"] = steady
+        if (pw > 1 and args.plan == "cost") or args.cell_split or (pw == 1 and args.single_tiles == "cost"):
+            out["config"]["calibration_frames"] = calib_frames(args)  # orbit positions, all before the timed ones
         if check is not None:
             out["check_mismatched_pixels"] = check
         n1 = live_ctr["n_rays"]
         out["single_frame"] = {"kernel_ms": round(kern_ms, 4), "mrays_s": round(n1 / kern_ms / 1e3, 1),
                                "camera": "app", "rays": n1, "variant": VARIANT_NAMES.get(roof_variant, roof_variant)}
-        # roofline of the timed launches themselves: algorithmic bytes of each launch (its frames x
-        # this rank's rays per frame x bytes per ray) / that launch's duration (HIP events on its
-        # stream around it), averaged over the timed launches -- the same launches rocprofv3's
-        # kernel trace of this command lists
+        # roofline. HBM: the bytes HBM actually moved (PMC, per timed launch of this
+        # command's shape, per frame) over the measured time per frame -- the kernel's real HBM
+        # fraction. Algorithmic models beside it: the compulsory bytes (outputs + one read of the
+        # scene per launch) and the clustered scan's own-work bytes per ray at chip level (cache-level
+        # traffic: above the HBM peak, which is why it cannot be the HBM fraction). VALU: the binding
+        # resource, wave-instructions issued per second against the chip's issue peak.
         clustered = args.variant in ("auto", "cl", "ps", "flat", "hyb")
         bpr = cluster_bytes_per_ray(live_ctr) if clustered else algorithmic_bytes_per_ray(live_ctr)
-        per_launch = [bpr * nf * local_rays_per_frame / (ms * 1e-3) / 1e9 for nf, ms in zip(launch_frames, launch_ms)]
-        achieved = float(np.mean(per_launch))
-        sf_achieved = bpr * n1 / (kern_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel_ms": round(float(np.mean(launch_ms)), 4), "launch_ms": [round(x, 3) for x in launch_ms],
-                "frames_per_launch": launch_frames, "concurrent_launches": S_,
-                "rays_per_launch": round(float(np.mean(launch_frames)) * local_rays_per_frame),
-                "bytes_per_ray": round(bpr, 1),
-                "model": "clustered scan, own work (DESIGN.md 6)" if clustered else "reference work (SURVEY.md 8(d))",
-                "single_frame_launch": {"kernel_ms": round(kern_ms, 4), "achieved": round(sf_achieved, 1),
-                                        "frac": round(sf_achieved / HBM_PEAK_GBS, 4), "rays": n1}}
+        step_s = elapsed / args.steps
+        fpl = max(launch_frames)
+        out_bytes = (4 + 4) * (own if pw > 1 else W * H)  # framebuffer + ray_casts, u32 each, per frame
+        scene_bytes = prep["scene_device_bytes"]
+        compulsory = out_bytes + scene_bytes / fpl
+        roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": None, "variant": None,
+                "ms_per_frame": round(step_s * 1e3, 4), "frames_per_launch": launch_frames,
+                "launch_ms": [round(x, 3) for x in launch_ms], "concurrent_launches": S_,
+                "compulsory": {"bytes_per_frame": round(compulsory), "achieved": round(compulsory / step_s / 1e9, 1),
+                               "frac": round(compulsory / step_s / 1e9 / HBM_PEAK_GBS, 5),
+                               "model": "outputs (framebuffer + ray_casts, 8 B/px) + the scene read once per launch"},
+                "own_work": {"bytes_per_ray": round(bpr, 1), "achieved_chip": round(bpr * rays_total / args.steps / world
+                                                                                      / step_s / 1e9, 1),
+                             "model": ("clustered scan, own work (DESIGN.md §6): L1/LDS/L2-level bytes"
+                                       if clustered else "reference work (SURVEY.md 8(d))")},
+                "single_frame_launch": {"kernel_ms": round(kern_ms, 4), "rays": n1}}
         gname = GOLDEN_COUNTERS.get(args.config)
-        if gname:  # the reference algorithm's bytes for the same rays, at this kernel's speed
+        if gname:  # the reference algorithm's bytes per ray for the same rays
             with open(os.path.join(ROOT, "tests", "golden", "goldens.json")) as f:
                 ctr = json.load(f)["hits"][gname]["counters"]
-            rbpr = algorithmic_bytes_per_ray(ctr)
-            roof["ref_bytes_per_ray"] = round(rbpr, 1)
-            roof["ref_equivalent_GBs"] = round(rbpr / bpr * achieved, 1)
-        # AUTO: CLUSTER cells for primary-only renders, FLAT cells otherwise (both render_kernel)
+            roof["own_work"]["ref_bytes_per_ray"] = round(algorithmic_bytes_per_ray(ctr), 1)
         kname = "persist_kernel" if args.variant == "ps" else "render_kernel"
         roof["kernel"] = kname
         roof["variant"] = VARIANT_NAMES.get(roof_variant, roof_variant)
+        # default: the compulsory model (no counters); replaced by the PMC-measured bytes below
+        roof["achieved"] = roof["compulsory"]["achieved"]
+        roof["frac"] = roof["compulsory"]["frac"]
+        roof["traffic"] = None
+        roof["source"] = "compulsory bytes (no PMC)"
         if world == 1 and not args.no_pmc:
-            traffic, why = pmc_traffic(args, kname, int(max(launch_frames)))
-            roof["traffic"] = traffic
-            roof["traffic_note"] = why
+            pmc, grid, why = pmc_counters(args, kname)
+            roof["pmc_note"] = why
+            if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+                # FETCH_SIZE doubled (MI355X_MICROARCH.md, HBM: gfx950 reports half the bytes of wide
+                # reads), both in KB; L2 <-> fabric bytes, Infinity-Cache hits included
+                traffic = 2.0 * pmc["FETCH_SIZE"] * 1024.0 + pmc["WRITE_SIZE"] * 1024.0
+                per_frame = traffic / fpl
+                roof["traffic"] = round(traffic)
+                roof["traffic_per_frame"] = round(per_frame)
+                roof["pmc_launch"] = {"frames": fpl, "grid_size": grid,
+                                      "fetch_bytes": round(2.0 * pmc["FETCH_SIZE"] * 1024.0),
+                                      "write_bytes": round(pmc["WRITE_SIZE"] * 1024.0)}
+                roof["achieved"] = round(per_frame / step_s / 1e9, 2)
+                roof["frac"] = round(per_frame / step_s / 1e9 / HBM_PEAK_GBS, 5)
+                roof["source"] = "PMC bytes of one timed-shape launch / frames / measured time per frame"
+            if pmc and "SQ_INSTS_VALU" in pmc:
+                valu_frame = pmc["SQ_INSTS_VALU"] / fpl
+                roof["valu"] = {"bound": "valu-issue", "wave_insts_per_frame": round(valu_frame),
+                                "achieved": round(valu_frame / step_s / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+                                "unit": "G wave-instr/s", "frac": round(valu_frame / step_s / VALU_ISSUE_PEAK, 4),
+                                "wait_frac": round(pmc.get("SQ_WAIT_ANY", 0.0) / max(1.0, pmc.get("SQ_WAVE_CYCLES", 1.0)), 4),
+                                "waves_per_frame": round(pmc.get("SQ_WAVES", 0.0) / fpl)}
+            if pmc and "TCC_HIT_sum" in pmc:
+                h, m = pmc["TCC_HIT_sum"], pmc.get("TCC_MISS_sum", 0.0)
+                roof["l2_hit_rate"] = round(h / max(1.0, h + m), 4)
         out["roofline"] = roof
         out["prep"] = prep
         if world == 1 and not args.no_cpu_baseline:

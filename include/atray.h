@@ -240,17 +240,17 @@ int atr_render_start_frames(atr_ctx* ctx, const atr_camera* cam, const atr_tile*
 int atr_render_start_cameras(atr_ctx* ctx, const atr_camera* cams, int32_t nframes, const atr_tile* tiles,
                              int32_t ntiles, const atr_frame* frame, int64_t frame_stride, uint64_t seed,
                              void* stream, int32_t variant);
-/* Diagnostic, synchronous: an instrumented render of the same work that returns
-   [0] traced rays, [1] box tests, [2] triangle tests, [3] leaves scanned -- the reference's own
-   per-ray work on this input (kd_tree.cpp:337-465) for every variant but CLUSTER, whose [2]
-   counts the full triangle tests it still runs -- and the engine's [4] wave-level triangle
-   iterations, [5] DFS passes, [6] all octree box tests, [7] wavefronts, [8] cluster boxes tested
-   and [9] primitives screened by the clustered scan. */
 /* Load-balance calibration, synchronous: renders `tiles` once (default kernel) and returns the
    GPU shader clocks spent per tile (sum over the 8x8 blocks whose area first falls in the tile,
    list order). Used to deal shard tiles to GPUs by measured cost (atray_amd/shard.py). */
 int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                           uint64_t seed, int64_t* cost_out);
+/* Diagnostic, synchronous: an instrumented render of the same work that returns
+   [0] traced rays, [1] box tests, [2] triangle tests, [3] leaves scanned -- the reference's own
+   per-ray work on this input (kd_tree.cpp:337-465) for every variant but the clustered ones,
+   whose [2] counts the full triangle tests they still run -- and the engine's [4] wave-level
+   triangle iterations, [5] DFS passes, [6] all octree box tests, [7] wavefronts, [8] cluster
+   boxes tested and [9] primitives screened by the clustered scan. */
 int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         uint64_t seed, int32_t variant, int64_t counters_out[10]);
 /* Diagnostic: one instrumented render; out = wave clocks (s_memtime, summed over waves) spent in
@@ -266,6 +266,12 @@ int atr_render_phase_clocks(atr_ctx* ctx, const atr_camera* cam, const atr_tile*
    them. out[3 + k] / (64 out[k]) is the lane utilisation of bounce bucket k. */
 int atr_render_path_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                              uint64_t seed, int32_t variant, int64_t out[6]);
+/* Diagnostic: one instrumented render; SIMD efficiency of the clustered scans: out[0] wave-level
+   iterations of the full-test candidate loops (two tests each in the paired loops), out[1] full
+   triangle tests, out[2] / out[3] DFS loop iterations at wave / lane level, out[4] dealt rounds,
+   out[5] the (ray, cluster) items they carried, out[6] traced rays. */
+int atr_render_simd_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
+                             uint64_t seed, int32_t variant, int64_t out[7]);
 /* Diagnostic: one render of `tiles` recording, per 8x8 work block (block order), the wave's start
    and end on the 100 MHz device clock and its HW_ID | XCC_ID << 32. out = 3 u64 per block;
    with out == NULL (or cap too small) only *nblocks is set. */

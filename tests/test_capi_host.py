@@ -213,3 +213,14 @@ def test_write_bmp_id_limit_and_errors(tmp_path):
     with pytest.raises(ValueError):
         E.write_bmp(np.zeros(4, np.uint32), base)
     assert E.lib().atr_write_bmp(None, 1, 1, b"x", None, 0) == -1  # ATR_E_INVALID
+
+
+def test_default_tuning_is_the_measured_schedule():
+    """atr_default_tuning (host-only): the knobs a context starts with."""
+    import ctypes as C
+    t = E.atr_tuning()
+    E.lib().atr_default_tuning(C.byref(t))
+    got = {f: getattr(t, f) for f, _ in E.atr_tuning._fields_ if f != "reserved"}
+    assert got == {"xcd_chunk": 16, "frame_rotate": 0, "hybrid_a": 2, "hybrid_b": 1, "persist_chunk": 16,
+                   "cluster_size": 16}
+    assert list(t.reserved) == [0] * 6

@@ -100,7 +100,7 @@ C5_BANDS = [(1112, 1114), (626, 627)]
 @pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
                                      E.ATR_KERNEL_HYBRID])
 def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
-    """C4 through AUTO (= FLAT for multi-bounce, capi.cpp auto_sched), CLUSTER and FLAT."""
+    """C4 through AUTO (= FLAT for multi-bounce, capi.cpp auto_sched), CLUSTER, PERSIST and HYBRID."""
     o = render(eng, E.camera(1920, 1080, 64, 5), variant)
     hitpx = sum(check_band(o, oracle_scene, O.Camera(1920, 1080, spp=64, bounces=5), a, b) for a, b in C4_BANDS)
     assert hitpx > 2000  # the bands cross the dragon

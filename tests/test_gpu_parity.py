@@ -22,6 +22,9 @@ SKY, MODEL = O.SKY, O.MODEL_MAT
 VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID]
 if os.environ.get("ATR_TEST_ALL_VARIANTS") == "1":
     VARIANTS += [E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8, E.ATR_KERNEL_WAVEFRONT]
+# ATR_TEST_VARIANTS=a,b,...: exactly these kernel codes (experiment builds and diagnostic schedules)
+if os.environ.get("ATR_TEST_VARIANTS"):
+    VARIANTS = [int(v) for v in os.environ["ATR_TEST_VARIANTS"].split(",")]
 RGB_RTOL = 1e-5
 
 
@@ -220,6 +223,38 @@ def test_cell_plan_changes_no_output(eng, variant):
         eng.set_cell_plan(W, H, np.full(((W + 7) // 8) * ((H + 7) // 8), 3, np.uint8))
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_tuning_changes_no_output(eng, variant):
+    """atr_set_tuning: XCD chunking, the HYBRID deal rule forced to always / never deal, the
+    PERSIST queue chunk and the cluster size (re-upload) change scheduling only -- every output
+    identical, primary and multi-bounce."""
+    W, H = 480, 270
+    base = eng.tuning()
+    settings = [{"xcd_chunk": 0}, {"xcd_chunk": 3}, {"hybrid_a": -4096, "hybrid_b": -4096},
+                {"hybrid_a": 4096, "hybrid_b": 4096}, {"persist_chunk": 1}, {"cluster_size": 7}]
+    try:
+        for spp, bounces in ((1, 1), (2, 3)):
+            upload(eng, "Dragon", True)
+            cam = E.camera(W, H, spp, bounces)
+            want = run(eng, cam, variant=variant)
+            for kw in settings:
+                eng.set_tuning(**kw)
+                upload(eng, "Dragon", True)  # cluster_size applies at upload
+                got = run(eng, cam, variant=variant)
+                eng.set_tuning(**base)
+                for k in ("fb", "face", "t", "casts", "rgb"):
+                    assert np.array_equal(np.asarray(want[k]).view(np.uint32), np.asarray(got[k]).view(np.uint32)), (kw, k)
+                assert want["traced"] == got["traced"], kw
+    finally:
+        eng.set_tuning(**base)
+        upload(eng, "Dragon", True)
+    with pytest.raises(E.AtrError):
+        eng.set_tuning(cluster_size=17)
+    with pytest.raises(E.AtrError):
+        eng.set_tuning(xcd_chunk=-1)
+    assert eng.tuning() == base
+
+
 def test_renderer_api_start_wait(eng):
     """renderer.h's start/wait pair over the engine, app-scene materials (app.cpp:91-131)."""
     from atray_amd import renderer as R
@@ -405,7 +440,8 @@ def test_gpu_work_counters_equal_reference_work(eng, name, variant):
     c = eng.counters(E.camera(g["W"], g["H"]), [[0, 0, g["W"] - 1, g["H"] - 1]], SEED, variant)
     for k in ["n_rays", "n_box", "n_leaf"]:
         assert c[k] == g["counters"][k], (k, c[k], g["counters"][k])
-    if variant in (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID) and g["tree"]:
+    exact_work = (E.ATR_KERNEL_LANE, E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8, E.ATR_KERNEL_WAVEFRONT)
+    if variant not in exact_work and g["tree"]:
         # the clustered scan visits the same leaves but skips provably irrelevant triangles
         assert 0 < c["n_tri"] <= g["counters"]["n_tri"], (c["n_tri"], g["counters"]["n_tri"])
     else:

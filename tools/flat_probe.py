@@ -56,8 +56,16 @@ for v in variants:
             n = max(1, ctr["n_rays"])
             row["per_ray"] = {k: round(val / n, 3) for k, val in ctr.items()}
             row["path"] = eng.path_counters(cam, tiles, SEED, v)
+            row["simd"] = eng.simd_counters(cam, tiles, SEED, v)
         out["runs"].append(row)
         print(json.dumps(row), flush=True)
 c3 = E.camera(W, H)
 out["c3_hybrid_ms"] = round(timed(c3, E.ATR_KERNEL_HYBRID), 3)
+out["c3_hybrid_simd"] = eng.simd_counters(c3, tiles, SEED, E.ATR_KERNEL_HYBRID)
+if os.environ.get("PHASES"):  # library built with -DATR_PHASE_CLOCKS (ATRAY_LIB)
+    for name, cam, v in (("c3_hybrid", c3, E.ATR_KERNEL_HYBRID), ("c4_flat", E.camera(W, H, spp, 5), variants[0])):
+        eng.phase_clocks(cam, tiles, SEED, v)
+        p = eng.phase_clocks(cam, tiles, SEED, v)
+        out["phases_" + name] = {**p, **{k + "_frac": round(p[k] / max(1, p["wave"]), 3)
+                                         for k in ("pass", "lane_private", "dealt", "step_prep", "scan")}}
 print(json.dumps(out), flush=True)
