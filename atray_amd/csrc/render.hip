@@ -11,6 +11,8 @@
 //         in its own order, so results are identical.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cluster.h"
 #include "shade.h"
 #include "trace.h"
@@ -789,6 +791,8 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                 // the camera rays of a bounce loop (one origin, coherent) take HYBRID's primary flavour
                 if (first)
                     tree_closest_flat<COUNT, true, true, false, true, true, false, CC>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                else if constexpr (SCHED == SCHED_FLAT)  // LDS leaf buffer: fewer VGPRs, 5 waves/SIMD (§4d)
+                    tree_closest_flat<COUNT, false, true, true, false, false, false, true>(r, m, active, h, err, ct);
                 else if constexpr (SCHED == SCHED_FLAT_UT)
                     tree_closest_flat<COUNT, false, true, true, false, true, false, CC>(r, m, active, h, err, ct);
                 else tree_closest_flat<COUNT, false, false, true, false, false, false, CC>(r, m, active, h, err, ct);
@@ -833,8 +837,13 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
 // sums, throughput, PCG state and counters are dead during the tree query, so a lane-private LDS
 // column holds them instead of registers the query needs (16 KB per 4-wave workgroup).
 constexpr int kStash = 16;
-__device__ __forceinline__ void stash_put(uint32_t* L, int k, float v) { L[64 * k] = __float_as_uint(v); }
-__device__ __forceinline__ float stash_getf(const uint32_t* L, int k) { return __uint_as_float(L[64 * k]); }
+// The stash lives in LDS (a lane-private column, stride 64 words) or, for FLAT, in the lane's
+// private (scratch) memory: a volatile local array, which the compiler must keep in memory (stride
+// 1), so the kernel's LDS is only the scan's 22.5 KB and more workgroups fit a CU.
+template <int ST, class PT>
+__device__ __forceinline__ void stash_put(PT* L, int k, uint32_t v) { L[ST * k] = v; }
+template <int ST, class PT>
+__device__ __forceinline__ uint32_t stash_get(PT* L, int k) { return L[ST * k]; }
 
 template <int SCHED, bool COUNT>
 __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d, int32_t bounce_limit,
@@ -842,8 +851,14 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
                                        int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b, V3& acc) {
     constexpr bool STASH = sched_flat(SCHED) || sched_hyb(SCHED);
-    __shared__ uint32_t s_stash[STASH ? 4 : 1][kStash][64];
-    uint32_t* L = &s_stash[STASH ? threadIdx.x >> 6 : 0][0][threadIdx.x & 63];
+    constexpr bool PRIV = SCHED == SCHED_FLAT;  // the stash in private memory (above)
+    constexpr int ST = PRIV ? 1 : 64;
+    __shared__ uint32_t s_stash[STASH && !PRIV ? 4 : 1][PRIV ? 1 : kStash][64];
+    volatile uint32_t pstash[PRIV ? kStash : 1];
+    using PT = std::conditional_t<PRIV, volatile uint32_t, uint32_t>;
+    PT* L;
+    if constexpr (PRIV) L = pstash;
+    else L = &s_stash[STASH ? threadIdx.x >> 6 : 0][0][threadIdx.x & 63];
     V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
     int32_t i = 0;
     bool live = active;
@@ -864,21 +879,26 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
         Isect id;
         id.type = T_NONE;
         if constexpr (STASH) {
-            stash_put(L, 0, ret.x); stash_put(L, 1, ret.y); stash_put(L, 2, ret.z);
-            stash_put(L, 3, w.x); stash_put(L, 4, w.y); stash_put(L, 5, w.z);
-            stash_put(L, 6, acc.x); stash_put(L, 7, acc.y); stash_put(L, 8, acc.z);
-            L[64 * 9] = uint32_t(st); L[64 * 10] = uint32_t(st >> 32);
-            L[64 * 11] = casts; L[64 * 12] = traced; L[64 * 13] = hit_face; stash_put(L, 14, hit_t);
+            stash_put<ST>(L, 0, __float_as_uint(ret.x)); stash_put<ST>(L, 1, __float_as_uint(ret.y));
+            stash_put<ST>(L, 2, __float_as_uint(ret.z)); stash_put<ST>(L, 3, __float_as_uint(w.x));
+            stash_put<ST>(L, 4, __float_as_uint(w.y)); stash_put<ST>(L, 5, __float_as_uint(w.z));
+            stash_put<ST>(L, 6, __float_as_uint(acc.x)); stash_put<ST>(L, 7, __float_as_uint(acc.y));
+            stash_put<ST>(L, 8, __float_as_uint(acc.z));
+            stash_put<ST>(L, 9, uint32_t(st)); stash_put<ST>(L, 10, uint32_t(st >> 32));
+            stash_put<ST>(L, 11, casts); stash_put<ST>(L, 12, traced); stash_put<ST>(L, 13, hit_face);
+            stash_put<ST>(L, 14, __float_as_uint(hit_t));
             __asm__ volatile("" ::: "memory");  // the values below come back from LDS
         }
         intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct, hyb_a, hyb_b, i == 0);
         if constexpr (STASH) {
             __asm__ volatile("" ::: "memory");
-            ret = mk(stash_getf(L, 0), stash_getf(L, 1), stash_getf(L, 2));
-            w = mk(stash_getf(L, 3), stash_getf(L, 4), stash_getf(L, 5));
-            acc = mk(stash_getf(L, 6), stash_getf(L, 7), stash_getf(L, 8));
-            st = uint64_t(L[64 * 9]) | (uint64_t(L[64 * 10]) << 32);
-            casts = L[64 * 11]; traced = L[64 * 12]; hit_face = L[64 * 13]; hit_t = stash_getf(L, 14);
+            auto gf = [&](int k) { return __uint_as_float(stash_get<ST>(L, k)); };
+            ret = mk(gf(0), gf(1), gf(2));
+            w = mk(gf(3), gf(4), gf(5));
+            acc = mk(gf(6), gf(7), gf(8));
+            st = uint64_t(stash_get<ST>(L, 9)) | (uint64_t(stash_get<ST>(L, 10)) << 32);
+            casts = stash_get<ST>(L, 11); traced = stash_get<ST>(L, 12); hit_face = stash_get<ST>(L, 13);
+            hit_t = gf(14);
         }
         if (!go) continue;
         ++traced;
@@ -1112,16 +1132,14 @@ ATR_INST(SCHED_FLAT_NOCC, false, false) ATR_INST(SCHED_FLAT_NOCC, true, false)
 ATR_INST(SCHED_FLAT_UT, false, false) ATR_INST(SCHED_FLAT_UT, true, false)
 ATR_INST(SCHED_HYBRID_NOCC, true, true) ATR_INST(SCHED_HYBRID_NOCC, true, false)
 ATR_INST(SCHED_HYBRID_NOCC, false, false)
+
 template __global__ void render_kernel<SCHED_HYBRID_NOCC, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 7>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, false, 5>(RenderParams);
-template __global__ void render_kernel<SCHED_FLAT, false, true, 5>(RenderParams);
-template __global__ void render_kernel<SCHED_FLAT, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, false, 5>(RenderParams);
-template __global__ void render_kernel<SCHED_FLAT, false, false, 3>(RenderParams);
-template __global__ void render_kernel<SCHED_FLAT, false, false, 2>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT, false, false, 6>(RenderParams);
 #undef ATR_INST4
 #undef ATR_INST
 template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
@@ -1232,7 +1250,8 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing;
     const dim3 g((P.nblocks + 3) / 4), b(256);
     if (sched >= 96) {  // diagnostic: 96 FLAT and 97 HYBRID without candidate compaction (round 2),
-                        // 100 FLAT with wave-walked DFS passes on every bounce
+                        // 100 FLAT with wave-walked DFS passes on every bounce (FLAT at n waves/SIMD:
+                        // 64 + n)
         if (sched == 96) {
             if (prim) return hipErrorInvalidValue;
             if (count) launch_one<atr::SCHED_FLAT_NOCC, true, false>(P, s);
@@ -1259,13 +1278,10 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
         else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
         return hipGetLastError();
     }
-    if (sched >= 64) {  // FLAT at 64 + n waves/SIMD (diagnostic)
+    if (sched >= 64) {  // FLAT bounce loops at 64 + n waves/SIMD (diagnostic: 4, 5, 6)
         const int o = sched - 64;
-        if (!count && o == 5 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 5>), g, b, 0, s, P);
-        else if (!count && o == 5) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
-        else if (!count && o == 6 && prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, true, 6>), g, b, 0, s, P);
-        else if (!count && o == 3 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 3>), g, b, 0, s, P);
-        else if (!count && o == 2 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 2>), g, b, 0, s, P);
+        if (!count && o == 6 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 6>), g, b, 0, s, P);
+        else if (!count && o == 5 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
         else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
         return hipGetLastError();
     }
@@ -1296,7 +1312,11 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     }
     switch (sched) {
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
-        case 6: launch_sched<atr::SCHED_FLAT>(P, count, prim, s); break;
+        case 6:  // bounce loops at 5 waves/SIMD (the LDS leaf buffer and private path stash let them fit:
+                 // 22.5 KB LDS, <= 102 VGPRs)
+            if (!prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
+            else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
+            break;
         case 7:  // primaries at 6 waves/SIMD (80 VGPRs; measured: DESIGN.md §4e)
             if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 6>), g, b, 0, s, P);
             else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);

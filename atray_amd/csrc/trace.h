@@ -297,10 +297,19 @@ __device__ __forceinline__ Inner load_inner_uniform(const float4_t* __restrict__
 // same f32 operations on the same operands as the reference's per-child slab test
 // (aabb.h:29-93), hence the same bits, computed once per node instead of per child and with
 // no child box loads. Child k: x half = k >> 2, y half = (k >> 1) & 1, z half = k & 1.
+// Descent cull: an inner child whose exit distance (its slab exit, z merged as aabb.h:29-63
+// computes it) is <= 0 or < bd holds no leaf the pass could insert -- every leaf below it is an
+// octant of an octant (bitwise, checked at upload), so its slab values lie between the child's
+// (b - o) * inv is monotone in b under f32 rounding) and its distance (entry, else exit, else 0)
+// is <= that exit: 0 (not inserted) or below the re-walk bound. The child still counts as hit for
+// the reference's 5-hit limit (kd_tree.cpp:374); only the walk into it is skipped. Valid when
+// no slab value can be NaN, i.e. 1/d is finite on every axis (`cull`, per ray); the rays it
+// helps are bounce rays, whose origins lie inside the tree and whose lines cross boxes behind
+// them (check_ray_AABB_intersection has no t > 0 test, aabb.h:65-93).
 template <int K, bool COUNT, class LB>
 __device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, LB& lb,
                                                   int32_t& ncand, float bd, int32_t bi, Ctr& ct,
-                                                  bool first_pass) {
+                                                  bool first_pass, bool cull = false) {
     const float X0 = (n.lx - r.o.x) * r.inv.x, X1 = (n.vx - r.o.x) * r.inv.x, X2 = (n.hx - r.o.x) * r.inv.x;
     const float Y0 = (n.ly - r.o.y) * r.inv.y, Y1 = (n.vy - r.o.y) * r.inv.y, Y2 = (n.hy - r.o.y) * r.inv.y;
     const float Z0 = (n.lz - r.o.z) * r.inv.z, Z1 = (n.vz - r.o.z) * r.inv.z, Z2 = (n.hz - r.o.z) * r.inv.z;
@@ -325,7 +334,8 @@ __device__ __forceinline__ uint32_t examine_inner(const Ray& r, const Inner& n, 
         if (!((n.bm >> i) & 1u)) {  // inner child: check_ray_AABB_intersection (aabb.h:65-93)
             if (in) {
                 ++nodes_hit;
-                mask |= 1u << i;
+                const float tx = tzmax < tmax ? tzmax : tmax;
+                if (!(cull && (tx <= 0.0f || tx < bd))) mask |= 1u << i;
             }
         } else {  // leaf child: get_ray_AABB_intersection (aabb.h:29-63)
             if (tzmin > tmin) tmin = tzmin;
@@ -358,8 +368,13 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
     if constexpr (COUNT) ct.pass += 1;
     lb_clear<K>(lb);
     int32_t ncand = 0;
+#ifdef ATR_NO_CULL
+    const bool cull = false;  // experiment build: the round-2 walk
+#else
+    const bool cull = isfinite(r.inv.x) && isfinite(r.inv.y) && isfinite(r.inv.z);
+#endif
     Inner cur = load_inner(tab, 0);
-    uint64_t lo = examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass);
+    uint64_t lo = examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull);
     uint64_t hi = 0;
     uint32_t bm = cur.bm;
     int32_t parent = -1, lvl = 0;
@@ -373,7 +388,7 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
             const uint32_t innerm = ~bm & ((1u << s) - 1u);  // inner children before s
             const int32_t id = int32_t(bm >> 8) + __popc(innerm);
             cur = load_inner(tab, id);
-            const uint64_t cm = examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass);
+            const uint64_t cm = examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull);
             ++lvl;
             if (lvl >= kMaskLevels) return -1;
             if (lvl < 8) lo |= cm << (8 * lvl);
@@ -405,8 +420,13 @@ __device__ __forceinline__ int32_t traverse_pass_wave(const Ray& r, const float4
     if constexpr (COUNT) { if (part) ct.pass += 1; }
     if (part) lb_clear<K>(lb);
     int32_t ncand = 0;
+#ifdef ATR_NO_CULL
+    const bool cull = false;  // experiment build: the round-2 walk
+#else
+    const bool cull = isfinite(r.inv.x) && isfinite(r.inv.y) && isfinite(r.inv.z);
+#endif
     Inner cur = load_inner_uniform(tab, 0);
-    uint64_t lo = part ? uint64_t(examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass)) : 0;
+    uint64_t lo = part ? uint64_t(examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull)) : 0;
     uint64_t hi = 0;
     uint32_t bm = cur.bm;  // wave-uniform walk state
     int32_t parent = -1, lvl = 0;
@@ -423,7 +443,7 @@ __device__ __forceinline__ int32_t traverse_pass_wave(const Ray& r, const float4
             const uint32_t innerm = ~bm & ((1u << s) - 1u);
             const int32_t id = int32_t(bm >> 8) + __popc(innerm);
             cur = load_inner_uniform(tab, id);
-            const uint64_t cm = act ? uint64_t(examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass)) : 0;
+            const uint64_t cm = act ? uint64_t(examine_inner<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull)) : 0;
             ++lvl;
             if (lvl >= kMaskLevels) return -1;
             if (lvl < 8) lo |= cm << (8 * lvl);
