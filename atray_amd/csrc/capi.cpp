@@ -36,6 +36,14 @@ extern "C" hipError_t atr_launch_packed_tile_casts(const int32_t* slot_tile, int
                                                    int64_t frame_stride, int32_t nframes, int32_t ntiles,
                                                    unsigned long long* out, hipStream_t s);
 
+extern "C" hipError_t atr_launch_plan(const atr::DBlock* base, int32_t nb, unsigned long long* cost,
+                                      unsigned long long* cost_last, void* work, atr::DBlock* out, int32_t max_split,
+                                      hipStream_t s);
+extern "C" size_t atr_plan_work_bytes(int32_t nb);
+extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s);
+extern "C" hipError_t atr_launch_scatter_bgr(const uint8_t* src, int64_t n, const int64_t* dst_index,
+                                             uint32_t* image, hipStream_t s);
+
 #define HIPCHK(x)                                      \
     do {                                               \
         hipError_t e_ = (x);                           \
@@ -65,6 +73,12 @@ struct BlockSet {
     // one event per stream that launched work reading this set, recorded after its latest such
     // launch: before the set's buffers are rewritten or freed, every one of them is waited for
     std::vector<std::pair<hipStream_t, hipEvent_t>> evs;
+    // single-frame plan (plan.hip): per-base-block clocks of the last single-frame launch, the
+    // planned block list built from them on the GPU, the stream that owns the pair
+    DevBuf cost, cost_last, plan_work, plan_blocks;
+    int32_t max_split = 0;
+    bool plan_ready = false;
+    hipStream_t plan_stream = nullptr;
 };
 
 // Device scratch freed on every exit path.
@@ -126,6 +140,7 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     out.clear();
     out.reserve(order.size());
     npix = 0;
+    bool classes = false;  // some cell has a dispatch class: blocks are reordered after the loop
     for (int32_t ci : order) {
         // cell plan (atr_set_cell_plan): a heavy cell is split into `parts` row bands, one wave
         // each, emitted back to back in lane order (the packed slot order does not change)
@@ -144,10 +159,19 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
             b.mask_lo = uint32_t(m);
             b.mask_hi = uint32_t(m >> 32);
             b.out_base = int32_t(npix);
+            b.flags = (pl & kPlanPrio) ? kBlockPrio : 0;
             npix += __builtin_popcountll(m);
             out.push_back(b);
+            if (pl & kPlanClassMask) classes = true;
         }
     }
+    if (classes) {  // dispatch order only: out_base keeps every block's packed slots
+        std::stable_sort(out.begin(), out.end(), [&](const DBlock& a, const DBlock& b) {
+            return (cplan[size_t(a.y0 / 8) * size_t(cw) + size_t(a.x0 / 8)] & kPlanClassMask) >
+                   (cplan[size_t(b.y0 / 8) * size_t(cw) + size_t(b.x0 / 8)] & kPlanClassMask);
+        });
+    }
+    for (size_t i = 0; i < out.size(); ++i) out[i].base = int32_t(i);
 }
 
 // IEEE binary16 bits of an integer |v| <= 2047 (exact).
@@ -174,6 +198,7 @@ atr_tuning default_tuning() {
     t.hybrid_b = 1;
     t.persist_chunk = 16;  // §4c
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
+    t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs
     return t;
 }
 constexpr int kSchedPersist = 8;
@@ -389,6 +414,7 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     }
     b.tiles.assign(tiles, tiles + ntiles);
     b.tile_ready = false;
+    b.plan_ready = false;
     b.width = W;
     b.height = H;
     b.cplan_gen = c->cplan_gen;
@@ -434,6 +460,17 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     return &b;
 }
 
+// Grow a device buffer to `bytes` (contents undefined when it grows; zeroed if `zero`).
+int ensure_buf(DevBuf& d, size_t bytes, bool zero) {
+    if (d.n >= bytes && d.p) return ATR_OK;
+    if (d.p) (void)hipFree(d.p);
+    d = DevBuf();
+    if (hipMalloc(&d.p, bytes) != hipSuccess) return ATR_E_NOMEM;
+    d.n = bytes;
+    if (zero && hipMemset(d.p, 0, bytes) != hipSuccess) return ATR_E_NOMEM;
+    return ATR_OK;
+}
+
 // variant (atray.h) -> kernel schedule (render.hip). AUTO = the measured fastest.
 int sched_of(int32_t variant) {
     switch (variant) {
@@ -457,6 +494,51 @@ int sched_of(int32_t variant) {
 int auto_sched(int32_t variant, const atr_camera& cam) {
     if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
     return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_HYBRID) : sched_of(ATR_KERNEL_FLAT);
+}
+
+// A single-frame launch of a cell schedule with the single-frame plan (tuning frame_plan, plan.hip):
+// the render dispatches the block list planned after the previous such launch of this tile list on
+// this stream (the base list the first time), adds each cell's clocks into the set's cost buffer,
+// and the plan kernels then build the next list from them. Another stream, a user cell plan for the
+// size or frame_plan 0 -> the plain base-list launch.
+// The render's completion events (ev_stop, ev_done) are recorded between the render and the plan
+// kernels, so atr_render_wait and atr_last_kernel_ms see the render alone.
+hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s);
+int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStream_t s) {
+    const int32_t nb = int32_t(bs->host.size());
+    const bool user_plan = !c->cplan.empty() && c->cplan_w == bs->width && c->cplan_h == bs->height;
+    const bool use = c->tune.frame_plan && !user_plan && nb > 0 && sched != kSchedPersist &&
+                     (!bs->plan_ready || bs->plan_stream == s);
+    if (!use) {
+        HIPCHK(launch_render(c, P, sched, s));
+        HIPCHK(hipEventRecord(c->ev_stop, s));
+        HIPCHK(hipEventRecord(c->ev_done, s));
+        return ATR_OK;
+    }
+    const int32_t max_split = std::max<int32_t>(1, nb / 25);  // spare blocks for splits (4 %)
+    int rc;
+    const bool fresh = !bs->cost.p;  // the buffers start zeroed; each plan leaves them zeroed
+    if ((rc = ensure_buf(bs->cost, size_t(nb) * sizeof(unsigned long long), true))) return rc;
+    if ((rc = ensure_buf(bs->cost_last, size_t(nb) * sizeof(unsigned long long), false))) return rc;
+    if ((rc = ensure_buf(bs->plan_work, atr_plan_work_bytes(nb), true))) return rc;
+    if ((rc = ensure_buf(bs->plan_blocks, size_t(nb + max_split) * sizeof(DBlock), false))) return rc;
+    if (!bs->plan_ready && !fresh)  // a rebuilt set reuses buffers a plan may not have cleared
+        HIPCHK(hipMemsetAsync(bs->cost.p, 0, size_t(nb) * sizeof(unsigned long long), s));
+    bs->max_split = max_split;
+    if (bs->plan_ready) {
+        P.blocks = static_cast<const DBlock*>(bs->plan_blocks.p);
+        P.nblocks = nb + max_split;
+    }
+    P.block_cost = static_cast<unsigned long long*>(bs->cost.p);
+    HIPCHK(launch_render(c, P, sched, s));
+    HIPCHK(hipEventRecord(c->ev_stop, s));
+    HIPCHK(hipEventRecord(c->ev_done, s));
+    HIPCHK(atr_launch_plan(static_cast<const DBlock*>(bs->dev.p), nb, static_cast<unsigned long long*>(bs->cost.p),
+                           static_cast<unsigned long long*>(bs->cost_last.p), bs->plan_work.p,
+                           static_cast<DBlock*>(bs->plan_blocks.p), max_split, s));
+    bs->plan_ready = true;
+    bs->plan_stream = s;
+    return ATR_OK;
 }
 
 // Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
@@ -776,7 +858,8 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
     if (!c || !t) return ATR_E_INVALID;
     if (t->xcd_chunk < 0 || t->xcd_chunk > 4096 || t->frame_rotate < 0 || t->frame_rotate > 1024 ||
         t->hybrid_a < -4096 || t->hybrid_a > 4096 || t->hybrid_b < -4096 || t->hybrid_b > 4096 ||
-        t->persist_chunk < 1 || t->persist_chunk > 4096 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize)
+        t->persist_chunk < 1 || t->persist_chunk > 4096 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
+        t->frame_plan < 0 || t->frame_plan > 1)
         return ATR_E_INVALID;
     for (int32_t r : t->reserved)
         if (r) return ATR_E_INVALID;
@@ -800,6 +883,8 @@ int atr_destroy(atr_ctx* c) {
         if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
         if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
         if (b.dev_tile.p) (void)hipFree(b.dev_tile.p);
+        for (DevBuf* d : {&b.cost, &b.cost_last, &b.plan_work, &b.plan_blocks})
+            if (d->p) (void)hipFree(d->p);
         for (auto& se : b.evs) (void)hipEventDestroy(se.second);
     }
     for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
@@ -1013,43 +1098,6 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 for (size_t cl = 0; cl < ncl; ++cl) {
                     std::memcpy(&blk[4 * kClusterBlock * cl], &C.rec[8 * cl], 8 * sizeof(float));
                     std::memcpy(&blk[4 * kClusterBlock * cl + 8], &nw[24 * cl], 24 * sizeof(uint32_t));
-                    // bounding spheres (cluster.h, sphere filter): centre as u8 steps of the box
-                    // extent per axis, radius in u8 steps of the largest extent, rounded so the
-                    // decoded sphere holds the triangle the test sees (a, a + ab, a + ac)
-                    const float* rc = &C.rec[8 * cl];
-                    uint32_t first, pw;
-                    std::memcpy(&pw, &rc[3], 4);
-                    std::memcpy(&first, &rc[7], 4);
-                    (void)first;
-                    const uint32_t n = (pw & 31u) + 1u;
-                    const double ext[3] = {double(rc[4]) - rc[0], double(rc[5]) - rc[1], double(rc[6]) - rc[2]};
-                    const double emax = std::max(ext[0], std::max(ext[1], ext[2]));
-                    for (uint32_t i = 0; i < n; ++i) {
-                        const size_t slot = cl * kMaxClusterSize + i;
-                        const float4_t q0 = s0[slot], q1 = s1[slot];
-                        const double a[3] = {q0.x, q0.y, q0.z};
-                        const double ab[3] = {q0.w, q1.x, q1.y}, ac[3] = {q1.z, q1.w, double(s2[slot].x)};
-                        const double v[3][3] = {{a[0], a[1], a[2]},
-                                                {a[0] + ab[0], a[1] + ab[1], a[2] + ab[2]},
-                                                {a[0] + ac[0], a[1] + ac[1], a[2] + ac[2]}};
-                        uint32_t u[3];
-                        double cen[3];
-                        for (int ax = 0; ax < 3; ++ax) {
-                            const double cc = (v[0][ax] + v[1][ax] + v[2][ax]) / 3.0;
-                            const double t = ext[ax] > 0 ? (cc - rc[ax]) / ext[ax] * 255.0 : 0.0;
-                            u[ax] = uint32_t(std::min(255.0, std::max(0.0, std::round(t))));
-                            cen[ax] = double(rc[ax]) + double(u[ax]) * (ext[ax] / 255.0);
-                        }
-                        double rr = 0;
-                        for (int j = 0; j < 3; ++j) {
-                            double d2 = 0;
-                            for (int ax = 0; ax < 3; ++ax) d2 += (v[j][ax] - cen[ax]) * (v[j][ax] - cen[ax]);
-                            rr = std::max(rr, std::sqrt(d2));
-                        }
-                        const double step = emax > 0 ? emax / 255.0 : 1.0;
-                        const uint32_t rq = uint32_t(std::min(255.0, std::ceil(rr / step * (1.0 + 1e-6)) + 1.0));
-                        blk[4 * kClusterBlock * cl + 32 + i] = u[0] | (u[1] << 8) | (u[2] << 16) | (rq << 24);
-                    }
                 }
                 if ((rc = dev_upload(c, blk.data(), blk.size() * sizeof(uint32_t), &p))) return rc;
                 dm.clus = static_cast<const float4_t*>(p);
@@ -1224,9 +1272,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     apply_tuning(c, P);
     const int wave = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
-    HIPCHK(launch_render(c, P, wave, s));
-    HIPCHK(hipEventRecord(c->ev_stop, s));
-    HIPCHK(hipEventRecord(c->ev_done, s));
+    if ((rc = launch_planned(c, bs, P, wave, s))) return rc;
     HIPCHK(note_launch(c, s, bs));
     c->have_render = true;
     c->last_stream = s;
@@ -1281,7 +1327,13 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
     apply_tuning(c, P);
     const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
-    if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
+    bool recorded = false;
+    if (sched != kSchedPersist && nframes == 1) {  // one frame: the single-frame plan applies
+        P.nblocks = nb;
+        P.frame_stride = frame_stride;
+        if ((rc = launch_planned(c, bs, P, sched, s))) return rc;
+        recorded = true;
+    } else if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
         P.nblocks = nb * nframes;
         P.frame_blocks = nb;
         P.frame_stride = frame_stride;
@@ -1304,8 +1356,10 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
             HIPCHK(launch_render(c, P, sched, s));
         }
     }
-    HIPCHK(hipEventRecord(c->ev_stop, s));
-    HIPCHK(hipEventRecord(c->ev_done, s));
+    if (!recorded) {
+        HIPCHK(hipEventRecord(c->ev_stop, s));
+        HIPCHK(hipEventRecord(c->ev_done, s));
+    }
     HIPCHK(note_launch(c, s, bs));
     c->have_render = true;
     c->last_stream = s;
@@ -1453,6 +1507,7 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     DevTmp cost;
     HIPCHK(hipMalloc(&fb.p, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
     HIPCHK(hipMalloc(&cost.p, std::max<size_t>(1, nb) * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(cost.p, 0, std::max<size_t>(1, nb) * sizeof(unsigned long long)));  // atomically added
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1465,7 +1520,7 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost.p);
     apply_tuning(c, P);
-    HIPCHK(atr_launch_render(P, sched_of(ATR_KERNEL_CLUSTER), nullptr));  // per-cell clocks
+    HIPCHK(atr_launch_render(P, auto_sched(ATR_KERNEL_AUTO, *cam), nullptr));  // per-cell clocks, AUTO's kernel
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
     if (nb) HIPCHK(hipMemcpy(h.data(), cost.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -1689,13 +1744,55 @@ int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles,
     return ATR_OK;
 }
 
+int atr_pack_bgr(atr_ctx* c, const uint32_t* framebuffer, int64_t npixels, uint8_t* out, void* stream) {
+    if (!c || npixels < 0 || (npixels && (!framebuffer || !out))) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(atr_launch_pack_bgr(framebuffer, npixels, out, static_cast<hipStream_t>(stream)));
+    return ATR_OK;
+}
+
+int atr_scatter_bgr(atr_ctx* c, const uint8_t* packed, int64_t npixels, const int64_t* dst_index, uint32_t* image,
+                    void* stream) {
+    if (!c || npixels < 0 || (npixels && (!packed || !dst_index || !image))) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(atr_launch_scatter_bgr(packed, npixels, dst_index, image, static_cast<hipStream_t>(stream)));
+    return ATR_OK;
+}
+
+int atr_render_plan_info(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width, int32_t height,
+                         int32_t* base_out, uint32_t* mask_hi_lo_out, int64_t cap, uint64_t* cost_out,
+                         int64_t* nplanned) {
+    if (!c || !nplanned || width <= 0 || height <= 0 || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, width, height, rc);
+    if (!bs) return rc;
+    *nplanned = 0;
+    if (!bs->plan_ready) return ATR_OK;
+    HIPCHK(wait_list(bs->evs));
+    const int64_t nb = int64_t(bs->host.size()), np = nb + bs->max_split;
+    *nplanned = np;
+    if (cap < np) return ATR_OK;  // size query
+    std::vector<DBlock> h(static_cast<size_t>(np));
+    HIPCHK(hipMemcpy(h.data(), bs->plan_blocks.p, size_t(np) * sizeof(DBlock), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < np; ++i) {
+        if (base_out) base_out[i] = h[size_t(i)].base;
+        if (mask_hi_lo_out) {
+            mask_hi_lo_out[2 * i] = h[size_t(i)].mask_lo;
+            mask_hi_lo_out[2 * i + 1] = h[size_t(i)].mask_hi;
+        }
+    }
+    if (cost_out) HIPCHK(hipMemcpy(cost_out, bs->cost_last.p, size_t(nb) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return ATR_OK;
+}
+
 int atr_set_cell_plan(atr_ctx* c, int32_t width, int32_t height, const uint8_t* plan) {
     if (!c || (plan && (width <= 0 || height <= 0))) return ATR_E_INVALID;
     const int32_t cw = (width + 7) / 8, ch = (height + 7) / 8;
     if (plan) {
         for (size_t i = 0; i < size_t(cw) * size_t(ch); ++i) {
             const int p = plan[i] & 0xF;
-            if ((plan[i] & 0xF0) || !(p == 0 || p == 1 || p == 2 || p == 4 || p == 8)) return ATR_E_INVALID;
+            if (!(p == 0 || p == 1 || p == 2 || p == 4 || p == 8)) return ATR_E_INVALID;
         }
         c->cplan.assign(plan, plan + size_t(cw) * size_t(ch));
         c->cplan_w = width;
@@ -1722,6 +1819,7 @@ int atr_render_cell_costs(atr_ctx* c, const atr_camera* cam, uint64_t seed, int3
     DevTmp cost;
     HIPCHK(hipMalloc(&fb.p, std::max<size_t>(1, size_t(bs->packed_pixels)) * 4));
     HIPCHK(hipMalloc(&cost.p, std::max<size_t>(1, nb) * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(cost.p, 0, std::max<size_t>(1, nb) * sizeof(unsigned long long)));  // atomically added
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;

@@ -35,8 +35,8 @@ constexpr int kMaxMaterials = 32;
 constexpr int kMaxFrameCams = 16;  // distinct cameras per multi-frame launch (kernel argument)
 constexpr int kMaxModels = 8;
 constexpr int kMaxClusterSize = 16;  // primitive slots per leaf cluster (ATR_CLUSTER_SIZE <= this)
-constexpr int kClusterBlock = 16;    // 16-B words per cluster block: record (2), screen normals (6),
-                                     // bounding spheres (4), spare (4)
+constexpr int kClusterBlock = 8;     // 16-B words per cluster block (one 128-B line): record (2),
+                                     // screen normals (6)
 
 struct V3 { float x, y, z; };
 ATR_HD V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -118,9 +118,8 @@ struct DModel {
     const uint32_t* tface;
     // leaf clusters, 2 float4 per cluster: {lo.xyz, bound of |ab||ac| with
     // (n - 1) in its low 5 mantissa bits}, {hi.xyz, q}; cl_range = first cluster, count per
-    // node. Cluster c owns the primitive slots [16 c, 16 c + n) and the 256-B block clus[16 c ..]:
-    // its record (2 words), then (cnrm = clus + 2) 6 words of its screen normals, then 4 words
-    // of bounding spheres (one u32 per slot: centre u8 x 3, radius u8)
+    // node. Cluster c owns the primitive slots [16 c, 16 c + n) and the 128-B block clus[8 c ..]:
+    // its record (2 words), then (cnrm = clus + 2) 6 words of its screen normals
     // n = ab x ac as f16 integer multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
     // c1 = {ab.yz, ac.xy}, c2 = {ac.z, bits(leaf rank)}, cface = face index
     const float4_t* clus;
@@ -158,9 +157,17 @@ struct alignas(16) DBlock {
     int32_t x0, y0;
     uint32_t mask_lo, mask_hi;
     int32_t out_base;  // PACKED layout: output slot of the block's first owned pixel
-    int32_t pad[3];
+    int32_t flags;     // kBlockPrio: the wave raises its issue priority (cell plan, atr_set_cell_plan)
+    int32_t base;      // index of the block in its tile list's base block list (per-block cost slot)
+    int32_t pad;
 };
 static_assert(sizeof(DBlock) == 32, "DBlock layout");
+constexpr int32_t kBlockPrio = 1;
+// cell plan byte (atr_set_cell_plan): low nibble = waves per cell (0/1, 2, 4, 8); bits 4-6 = the
+// cell's dispatch class (blocks of class 7 lead the block list, then 6, ..., 0; Morton order within
+// a class; their packed slots do not move); kPlanPrio = its waves issue at raised priority
+constexpr int kPlanClassShift = 4;
+constexpr uint8_t kPlanClassMask = 0x70, kPlanPrio = 0x80;
 
 // Per-render kernel argument (by value, no dynamic indexing into it).
 struct RenderParams {
@@ -181,7 +188,7 @@ struct RenderParams {
     unsigned long long* traced_rays;
     int32_t* error_flag;  // set to 1 if a ray hit a traversal limit (never for depth <= 16)
     unsigned long long* counters;  // non-null -> instrumented kernel (10 u64, see render.hip)
-    unsigned long long* block_cost;  // non-null -> shader clocks spent per block (load balance)
+    unsigned long long* block_cost;  // non-null -> shader clocks added per base block (blocks[b].base)
     unsigned long long* wave_trace;  // non-null -> per block: start, end (100 MHz clock), HW_ID | XCC_ID << 32
     int32_t xcd_chunk;  // 0: contiguous block range per XCD; k > 0: k-workgroup chunks dealt round-robin
     uint32_t* queue;    // PERSIST: 8 zeroed per-XCD work-queue heads (persist.hip)

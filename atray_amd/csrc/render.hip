@@ -423,7 +423,13 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     }
     uint32_t res_slot = 0xFFFFFFFFu;
     float res_t = kMaxFloat, res_u = 0.f, res_v = 0.f;
+#ifdef ATR_PRIO_STEPS
+    int32_t nsteps = 0;  // experiment: a wave still stepping after ATR_PRIO_STEPS steps issues first
+#endif
     for (;;) {
+#ifdef ATR_PRIO_STEPS
+        if (++nsteps == ATR_PRIO_STEPS) __builtin_amdgcn_s_setprio(2);
+#endif
         ATR_PCLK(const uint64_t tc0 = clock64());
         if constexpr (UT) {  // the wave walks its passes together (traverse_pass_wave)
             if (__ballot(need)) {
@@ -971,10 +977,11 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
                      P.frame_blocks);
     DBlock blk;
     if (in_range) blk = P.blocks[bi];
-    else { blk.x0 = 0; blk.y0 = 0; blk.mask_lo = 0; blk.mask_hi = 0; blk.out_base = 0; }
+    else { blk.x0 = 0; blk.y0 = 0; blk.mask_lo = 0; blk.mask_hi = 0; blk.out_base = 0; blk.flags = 0; blk.base = 0; blk.pad = 0; }
     const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
     const bool active = (mask >> lane) & 1;
     const int32_t x = blk.x0 + (lane & 7), y = blk.y0 + (lane >> 3);
+    if (__builtin_amdgcn_readfirstlane(blk.flags) & kBlockPrio) __builtin_amdgcn_s_setprio(2);  // cell plan
     const uint64_t clk0 = P.block_cost ? clock64() : 0;
     uint64_t clk1 = 0;
     if constexpr (COUNT) clk1 = clock64();
@@ -1057,7 +1064,8 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
         if (lane == 0 && t) atomicAdd(P.traced_rays + 16 * (b & 63), (unsigned long long)t);
     }
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
-    if (P.block_cost && lane == 0 && in_range) P.block_cost[b] = clock64() - clk0;
+    // per-cell cost (calibration, the single-frame plan): a split cell's waves add up
+    if (P.block_cost && lane == 0 && in_range && omask) atomicAdd(P.block_cost + ob.base, (unsigned long long)(clock64() - clk0));
     if (P.wave_trace && lane == 0 && in_range) {  // diagnostic: where and when this wave ran
         uint32_t hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -1317,8 +1325,11 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
             if (!prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
             else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
             break;
-        case 7:  // primaries at 6 waves/SIMD (80 VGPRs; measured: DESIGN.md §4e)
-            if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 6>), g, b, 0, s, P);
+        case 7:  // primaries: one frame at 6 waves/SIMD (its slowest cells set the latency), frames in
+                 // flight at 7 (72 VGPRs: throughput)
+            if (prim && !count && P.frame_blocks > 0)
+                hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 7>), g, b, 0, s, P);
+            else if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID, false, true, 6>), g, b, 0, s, P);
             else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
             break;
         case 2: launch_sched<atr::SCHED_TILE4>(P, count, prim, s); break;

@@ -19,6 +19,12 @@ LIB_PATH = os.environ.get("ATRAY_LIB") or os.path.join(HERE, "_lib", "libatray_h
 
 ATR_LAYOUT_IMAGE = 0
 ATR_LAYOUT_PACKED = 1
+ATR_PLAN_PRIO = 0x80  # cell plan: raised issue priority (atr_set_cell_plan)
+
+
+def plan_class(c):
+    """Cell plan dispatch class (ATR_PLAN_CLASS): class 7 cells are dispatched first, class 0 last."""
+    return (int(c) & 7) << 4
 ATR_KERNEL_AUTO, ATR_KERNEL_LANE, ATR_KERNEL_WAVE, ATR_KERNEL_TILE, ATR_KERNEL_TILE8 = 0, 1, 2, 3, 4
 ATR_KERNEL_WAVEFRONT = 5
 ATR_KERNEL_CLUSTER = 6
@@ -87,7 +93,7 @@ class atr_frame(C.Structure):
 class atr_tuning(C.Structure):
     _fields_ = [("xcd_chunk", C.c_int32), ("frame_rotate", C.c_int32), ("hybrid_a", C.c_int32),
                 ("hybrid_b", C.c_int32), ("persist_chunk", C.c_int32), ("cluster_size", C.c_int32),
-                ("reserved", C.c_int32 * 6)]
+                ("frame_plan", C.c_int32), ("reserved", C.c_int32 * 5)]
 
 
 # every symbol include/atray.h declares (checked by tests/test_capi_symbols.py)
@@ -104,7 +110,7 @@ EXPORTS = [
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_render_phase_clocks", "atr_render_path_counters", "atr_default_tuning", "atr_set_tuning",
-    "atr_get_tuning", "atr_render_simd_counters",
+    "atr_get_tuning", "atr_render_simd_counters", "atr_pack_bgr", "atr_scatter_bgr",
 ]
 
 _lib = None
@@ -162,6 +168,9 @@ def lib():
         "atr_default_tuning": ([P(atr_tuning)], None),
         "atr_set_tuning": ([vp, P(atr_tuning)], C.c_int),
         "atr_get_tuning": ([vp, P(atr_tuning)], C.c_int),
+        "atr_pack_bgr": ([vp, vp, i64, vp, vp], C.c_int),
+        "atr_render_plan_info": ([vp, vp, i32, i32, i32, vp, vp, i64, vp, P(i64)], C.c_int),
+        "atr_scatter_bgr": ([vp, vp, i64, vp, vp, vp], C.c_int),
         "atr_render_simd_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
@@ -531,6 +540,32 @@ class Engine:
         check(lib().atr_render_phase_clocks(self.h, C.byref(cam), C.cast(arr, C.c_void_p), n, C.c_uint64(seed),
                                             int(variant), out), "phase clocks")
         return dict(zip(["pass", "lane_private", "dealt", "wave", "step_prep", "scan"], list(out)))
+
+    def pack_bgr(self, fb_ptr, npixels, out_ptr, stream=None):
+        """BGRX u32 -> 3 bytes per pixel (atr_pack_bgr; device pointers, async on `stream`)."""
+        check(lib().atr_pack_bgr(self.h, C.c_void_p(fb_ptr), int(npixels), C.c_void_p(out_ptr),
+                                 C.c_void_p(stream) if stream else None), "pack bgr")
+
+    def scatter_bgr(self, packed_ptr, npixels, index_ptr, image_ptr, stream=None):
+        """3-byte pixels -> BGRX u32 at image[index[i]] (atr_scatter_bgr; device pointers, async)."""
+        check(lib().atr_scatter_bgr(self.h, C.c_void_p(packed_ptr), int(npixels), C.c_void_p(index_ptr),
+                                    C.c_void_p(image_ptr), C.c_void_p(stream) if stream else None), "scatter bgr")
+
+    def plan_info(self, tiles, width, height):
+        """The single-frame plan of a tile list (diagnostic): (base index per planned block, masks
+        (n, 2) u32, cost per base block) or None before the first planned launch."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        npl = C.c_int64()
+        args = (self.h, C.cast(arr, C.c_void_p), n, int(width), int(height))
+        check(lib().atr_render_plan_info(*args, None, None, 0, None, C.byref(npl)), "plan info")
+        if npl.value == 0:
+            return None
+        base = np.zeros(npl.value, np.int32)
+        masks = np.zeros((npl.value, 2), np.uint32)
+        cost = np.zeros(npl.value, np.uint64)  # the base list is shorter than the planned one
+        check(lib().atr_render_plan_info(*args, base.ctypes.data, masks.ctypes.data, npl.value, cost.ctypes.data,
+                                         C.byref(npl)), "plan info")
+        return base, masks, cost
 
     def tuning(self):
         """The context's scheduling knobs (atr_get_tuning) as a dict."""

@@ -142,21 +142,36 @@ def grid_tile_count(plan: ShardPlan) -> int:
     return (-(-plan.width // plan.side)) * (-(-plan.height // plan.side))
 
 
-def gather_frames(send, recv, plan: ShardPlan, rank: int, nframes: int, dist):
+def gather_frames(send, recv, plan: ShardPlan, rank: int, nframes: int, dist, unit: int = 1):
     """Exact-size gather of nframes packed frames to rank 0 (the one exchange step: RCCL send/recv
     over xGMI for backend "nccl"). `send`: this rank's frames back to back (nframes x size_r
-    elements; rank 0's own block is written in place by its render). `recv` (rank 0): the exact
-    gather buffer (frame_offsets with the launch's frame capacity F). Returns the async works."""
+    pixels; rank 0's own block is written in place by its render). `recv` (rank 0): the exact
+    gather buffer (frame_offsets with the launch's frame capacity F). `unit`: elements per pixel
+    (1: u32 BGRX; 3: the 3-byte BGR exchange, u8 tensors). Returns the async works."""
     ops = []
     if rank == 0:
-        off = frame_offsets(plan, recv.numel() // (plan.width * plan.height))
+        off = frame_offsets(plan, recv.numel() // (unit * plan.width * plan.height))
         for r in range(1, plan.world):
-            n = plan.sizes[r] * nframes
+            n = plan.sizes[r] * nframes * unit
             if n:
-                ops.append(dist.P2POp(dist.irecv, recv[off[r]:off[r] + n], r))
+                ops.append(dist.P2POp(dist.irecv, recv[unit * off[r]:unit * off[r] + n], r))
     elif plan.sizes[rank]:
-        ops.append(dist.P2POp(dist.isend, send[:plan.sizes[rank] * nframes], 0))
+        ops.append(dist.P2POp(dist.isend, send[:plan.sizes[rank] * nframes * unit], 0))
     return dist.batch_isend_irecv(ops) if ops else []
+
+
+def pack_bgr_host(fb) -> np.ndarray:
+    """Host reference of atr_pack_bgr: BGRX u32 pixels -> 3 bytes each (B, G, R); the X byte must
+    be 0 (texture.h:27-38), so nothing is lost."""
+    b = np.ascontiguousarray(np.asarray(fb, np.uint32)).view(np.uint8).reshape(-1, 4)
+    assert not b[:, 3].any(), "BGRX framebuffer with a nonzero X byte"
+    return np.ascontiguousarray(b[:, :3]).reshape(-1)
+
+
+def scatter_bgr_host(packed, dst_index, image) -> None:
+    """Host reference of atr_scatter_bgr: image[dst_index[i]] = B | G << 8 | R << 16."""
+    p = np.asarray(packed, np.uint8).reshape(-1, 3).astype(np.uint32)
+    image[np.asarray(dst_index, np.int64)] = p[:, 0] | (p[:, 1] << 8) | (p[:, 2] << 16)
 
 
 def scatter_host(bufs, plan: ShardPlan) -> np.ndarray:

@@ -276,6 +276,10 @@ def main():
                     help="N=1 tile list: one full-frame tile (default) or the shard grid, heaviest tiles first")
     ap.add_argument("--rank0-extra", type=float, default=0.05,
                     help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
+    ap.add_argument("--exchange", default="bgr", choices=["bgr", "bgrx"],
+                    help="N>1 frame exchange: 3 bytes per pixel (the framebuffer's X byte is always 0; "
+                         "atr_pack_bgr / atr_scatter_bgr) or the u32 BGRX framebuffer (gloo rehearsals always "
+                         "use bgrx)")
     ap.add_argument("--check", action="store_true",
                     help="rank 0: compare every assembled frame with a one-launch full-frame render")
     ap.add_argument("--sim-world", type=int, default=0,
@@ -338,14 +342,28 @@ def selftest(args):
             fb[f * own:(f + 1) * own] = pix + 7 * (k + f)
             casts[f] = pix % 5
         tsum = torch.zeros(F, ngrid, dtype=torch.int64).index_add_(1, stile, casts)
+        bgr = args.exchange == "bgr"
+        if bgr:  # the 3-byte exchange through the host references of atr_pack_bgr / atr_scatter_bgr
+            big3 = torch.zeros(3 * F * W * H, dtype=torch.uint8)
+            mine = torch.from_numpy(S.pack_bgr_host(fb[:F * own].numpy().astype(np.uint32)))
+            if rank == 0:
+                big3[3 * off[0]:3 * off[0] + 3 * F * own] = mine
         if world > 1:
-            works = S.gather_frames(fb, big, plan, rank, nf, dist)
+            if bgr:
+                works = S.gather_frames(mine, big3, plan, rank, nf, dist, unit=3)
+            else:
+                works = S.gather_frames(fb, big, plan, rank, nf, dist)
             works.append(dist.reduce(tsum, dst=0, async_op=True))
             for w_ in works:
                 w_.wait()
         if rank == 0:
             img = torch.zeros(F * W * H, dtype=torch.int64)
-            img.index_copy_(0, dst, big)
+            if bgr:
+                im = np.zeros(F * W * H, np.uint32)
+                S.scatter_bgr_host(big3.numpy(), dst.numpy(), im)
+                img = torch.from_numpy(im.astype(np.int64))
+            else:
+                img.index_copy_(0, dst, big)
             want = torch.arange(W * H, dtype=torch.int64)
             for f in range(nf):
                 got = img[f * W * H:(f + 1) * W * H]
@@ -360,6 +378,7 @@ def selftest(args):
                           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                           "data": "selftest: synthetic fill, no GPU", "selftest": True,
                           "config": {"workload": f"{args.config} plan/gather selftest {W}x{H}",
+                                     "exchange": args.exchange,
                                      "parallelism": f"tiles{world}", "shard_pixels": [int(x) for x in plan.sizes]},
                           "frames_checked": frames, "check_mismatched_pixels": mism,
                           "total_ray_casts_ok": bool(casts_ok)}), flush=True)
@@ -475,6 +494,7 @@ def run(args):
     own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
     npx = W * H
     on_host = world > 1 and backend != "nccl"
+    bgr = pw > 1 and args.exchange == "bgr" and not on_host  # 3-byte exchange (device kernels)
     traced = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
     # per stream slot: F framebuffers and F ray_casts images (u32), frames back to back
     casts = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
@@ -490,7 +510,18 @@ def run(args):
         tids = torch.from_numpy(S.tile_ids(plan, pr)).to(dev)
         tcasts = [torch.zeros(F_, max(1, len(tids)), dtype=torch.int64, device=dev) for _ in range(S_)]
         tsum = [torch.zeros(F_, ngrid, dtype=torch.int64, device="cpu" if on_host else dev) for _ in range(S_)]
-        if rank == 0 and not sim:
+        if bgr:
+            # 3-byte exchange: every rank packs its F frames into bytes (rank 0 straight into its
+            # block of the byte gather buffer), rank 0 scatters the gathered bytes into the images
+            fbs = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
+            if rank == 0 and not sim:
+                big = [torch.zeros(3 * F_ * npx, dtype=torch.uint8, device=dev) for _ in range(S_)]
+                dst_idx = torch.from_numpy(S.frames_assembly_index(plan, F_)).to(dev)
+                images = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
+                send3 = [b_[3 * off[0]:3 * off[0] + 3 * F_ * own] for b_ in big]
+            else:
+                send3 = [torch.zeros(3 * F_ * max(1, own), dtype=torch.uint8, device=dev) for _ in range(S_)]
+        elif rank == 0 and not sim:
             big = [torch.zeros(F_ * npx, dtype=torch.int32, device="cpu" if on_host else dev) for _ in range(S_)]
             dst_idx = torch.from_numpy(S.frames_assembly_index(plan, F_)).to(dev)
             images = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
@@ -525,7 +556,10 @@ def run(args):
         with torch.cuda.stream(streams[q]):
             for w_ in works:
                 w_.wait()
-            if rank == 0:
+            if rank == 0 and bgr:
+                eng.scatter_bgr(big[q].data_ptr(), big[q].numel() // 3, dst_idx.data_ptr(), images[q].data_ptr(),
+                                stream=streams[q].cuda_stream)
+            elif rank == 0:
                 src = big[q]
                 if on_host:
                     staging.copy_(src, non_blocking=False)
@@ -556,8 +590,15 @@ def run(args):
                         ts.index_copy_(1, tids.cpu(), part.cpu())
                     else:
                         ts.index_copy_(1, tids, part)
+                if bgr and own:  # the rank's frames in 3 bytes per pixel (part of its per-rank work)
+                    eng.pack_bgr(fbs[q].data_ptr(), nf * own, send3[q].data_ptr(), stream=streams[q].cuda_stream)
                 if sim:
                     pending[j] = (q, [])
+                    return
+                if bgr:
+                    works = S.gather_frames(send3[q], big[q] if rank == 0 else None, plan, rank, nf, dist, unit=3)
+                    works.append(dist.reduce(ts, dst=0, async_op=True))
+                    pending[j] = (q, works)
                     return
                 send = fbs[q]
                 if on_host:
@@ -715,6 +756,7 @@ def run(args):
                           "plan": (f"{args.plan}/{args.tile_order}" if pw > 1 else
                                    "single" if args.single_tiles == "frame" else f"single/{args.tile_order}"),
                           "streams": args.streams, "frames_per_launch": F_,
+                          **({"exchange": "bgr (3 B/px)" if bgr else "bgrx (4 B/px)"} if pw > 1 else {}),
                           "launches": launch_sizes(args.steps, F_, S_),
                           "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),
                           "cell_split": cell_split,

@@ -166,7 +166,12 @@ typedef struct {
                                cluster count exceeds a x rounds + b, -4096..4096; default 2, 1 */
     int32_t persist_chunk;  /* PERSIST: 8x8 cells per work-queue claim, 1..4096; default 16 */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
-    int32_t reserved[6];    /* must be 0 */
+    int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
+                               dispatches its tiles' cells by that launch's measured cost, heaviest
+                               first, the heaviest 1 % over two waves (built on the GPU after each
+                               such launch); 0: list order; default 1. Ignored while
+                               an atr_set_cell_plan plan is set for the image size */
+    int32_t reserved[5];    /* must be 0 */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
 int atr_set_tuning(atr_ctx* ctx, const atr_tuning* tuning);
@@ -299,12 +304,32 @@ int atr_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int3
 int atr_packed_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width,
                               int32_t height, const uint32_t* packed_ray_casts, int32_t nframes,
                               int64_t frame_stride, int64_t* out, void* stream);
+/* Multi-GPU frame exchange in 3 bytes per pixel (the framebuffer's X byte is always 0,
+   texture.h:27-38). atr_pack_bgr: npixels BGRX u32 -> 3 * npixels bytes (B, G, R per pixel).
+   atr_scatter_bgr: the inverse with a scatter, image[dst_index[i]] = B | G << 8 | R << 16 for
+   pixel i of `packed` (e.g. rank 0's gathered shard frames and their assembly index). Device
+   pointers; asynchronous on `stream`. */
+int atr_pack_bgr(atr_ctx* ctx, const uint32_t* framebuffer, int64_t npixels, uint8_t* out, void* stream);
+int atr_scatter_bgr(atr_ctx* ctx, const uint8_t* packed, int64_t npixels, const int64_t* dst_index, uint32_t* image,
+                    void* stream);
 /* Per-cell launch plan for renders of width x height (NULL clears): one byte per 8x8 cell (row
-   major, ceil(W/8) x ceil(H/8)): the number of waves the cell is split into (0/1 = one, 2, 4 or
-   8 row bands: a heavy cell's rays then share their dealt leaf scans with 2-8x as many lanes and
-   its dependent chain shortens). Only scheduling changes: outputs and the PACKED slot order are
-   identical with any plan. */
+   major, ceil(W/8) x ceil(H/8)). Low nibble: the number of waves the cell is split into (0/1 =
+   one, 2, 4 or 8 row bands: a heavy cell's rays then share their dealt leaf scans with 2-8x as
+   many lanes and its dependent chain shortens). Bits 4-6: the cell's dispatch class c (0-7):
+   cells of class 7 are dispatched first, then 6, ..., then 0 (list order within a class), e.g.
+   the heaviest cells of the previous frame first (ATR_PLAN_CLASS(c) = c << 4). ATR_PLAN_PRIO:
+   its waves issue at raised priority on their SIMD. Only scheduling changes: outputs and the
+   PACKED slot order are identical with any plan. */
+#define ATR_PLAN_CLASS(c) ((uint8_t)(((c) & 7) << 4))
+enum { ATR_PLAN_PRIO = 0x80 };
 int atr_set_cell_plan(atr_ctx* ctx, int32_t width, int32_t height, const uint8_t* plan);
+/* Diagnostic, synchronous: the single-frame plan of a tile list (tuning frame_plan): *nplanned =
+   the planned block list's length (0 = no plan yet; a size query when cap is too small); per
+   planned block its base block index (base_out) and lane mask (2 u32, lo then hi); cost_out = the
+   clocks per base block of the last measured launch (the base list's length). */
+int atr_render_plan_info(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32_t width, int32_t height,
+                         int32_t* base_out, uint32_t* mask_hi_lo_out, int64_t cap, uint64_t* cost_out,
+                         int64_t* nplanned);
 /* Measured cost (shader clocks) of every 8x8 cell of a full-frame render of `cam` with `variant`
    (cell kernels only): out has ceil(W/8) x ceil(H/8) entries, row major. Synchronous. */
 int atr_render_cell_costs(atr_ctx* ctx, const atr_camera* cam, uint64_t seed, int32_t variant,

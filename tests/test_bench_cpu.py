@@ -20,17 +20,17 @@ def _json_line(out):
     return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("n", [2, 3, 8])
-def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n):
+@pytest.mark.parametrize("n,exchange", [(2, "bgr"), (2, "bgrx"), (3, "bgr"), (8, "bgr")])
+def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n, exchange):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--selftest",
-                        "--steps", "11", "--warmup", "1", "--frames-per-launch", "4"],
+                        "--steps", "11", "--warmup", "1", "--frames-per-launch", "4", "--exchange", exchange],
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _json_line(r.stdout)
-    assert d["n_gpus"] == n and d["selftest"] is True
+    assert d["n_gpus"] == n and d["selftest"] is True and d["config"]["exchange"] == exchange
     assert d["frames_checked"] == 11
     assert d["check_mismatched_pixels"] == 0 and d["total_ray_casts_ok"] is True
     assert sum(d["config"]["shard_pixels"]) == 480 * 272

@@ -209,6 +209,10 @@ def test_cell_plan_changes_no_output(eng, variant):
             cost = eng.cell_costs(E.camera(W, H), SEED).ravel()
             plan = rng.choice(np.array([0, 1, 2, 4, 8], np.uint8), size=cost.size, p=[0.6, 0.1, 0.1, 0.1, 0.1])
             plan[np.argsort(-cost)[:40]] = 4
+            # dispatch-first and priority flags on random cells (scheduling only)
+            plan |= rng.choice(np.array([0, E.plan_class(7), E.plan_class(3), E.ATR_PLAN_PRIO,
+                                         E.plan_class(5) | E.ATR_PLAN_PRIO], np.uint8), size=cost.size,
+                               p=[0.6, 0.1, 0.1, 0.1, 0.1])
             eng.set_cell_plan(W, H, plan)
             got = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
                                                         variant=variant)]
@@ -221,6 +225,8 @@ def test_cell_plan_changes_no_output(eng, variant):
         eng.set_cell_plan(W, H, None)
     with pytest.raises(E.AtrError):
         eng.set_cell_plan(W, H, np.full(((W + 7) // 8) * ((H + 7) // 8), 3, np.uint8))
+    with pytest.raises(E.AtrError):
+        eng.set_cell_plan(W, H, np.full(((W + 7) // 8) * ((H + 7) // 8), 0x45, np.uint8))
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -231,7 +237,8 @@ def test_tuning_changes_no_output(eng, variant):
     W, H = 480, 270
     base = eng.tuning()
     settings = [{"xcd_chunk": 0}, {"xcd_chunk": 3}, {"hybrid_a": -4096, "hybrid_b": -4096},
-                {"hybrid_a": 4096, "hybrid_b": 4096}, {"persist_chunk": 1}, {"cluster_size": 7}]
+                {"hybrid_a": 4096, "hybrid_b": 4096}, {"persist_chunk": 1}, {"cluster_size": 7},
+                {"frame_plan": 0}]
     try:
         for spp, bounces in ((1, 1), (2, 3)):
             upload(eng, "Dragon", True)
@@ -253,6 +260,45 @@ def test_tuning_changes_no_output(eng, variant):
     with pytest.raises(E.AtrError):
         eng.set_tuning(xcd_chunk=-1)
     assert eng.tuning() == base
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_frame_plan_changes_no_output(eng, variant):
+    """The single-frame plan (tuning frame_plan, plan.hip): consecutive one-frame launches of a
+    tile list dispatch the cells by the previous launch's cost, heaviest first, the heaviest 1 %
+    split over two row-band waves -- image and packed layouts, primary and multi-bounce, every
+    output identical to the plain list order, launch after launch."""
+    upload(eng, "Dragon", True)
+    W, H = 480, 270
+    base = eng.tuning()
+    try:
+        for spp, bounces in ((1, 1), (2, 3)):
+            cam = E.camera(W, H, spp, bounces)
+            tiles = E.make_shard_tiles(W, H, 64, 1, 2)
+            eng.set_tuning(frame_plan=0)
+            want = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
+                                                         variant=variant)]
+            eng.set_tuning(frame_plan=1)
+            for _ in range(3):  # the first launch measures, the later ones dispatch by the plan
+                got = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
+                                                            variant=variant)]
+                for a, b in zip(want, got):
+                    for k in ("fb", "face", "t", "casts", "rgb"):
+                        assert np.array_equal(np.asarray(a[k]).view(np.uint32), np.asarray(b[k]).view(np.uint32)), k
+                    assert a["traced"] == b["traced"]
+        # costs that jump between launches (a sky view, then the dragon): the previous plan's
+        # thresholds would split far more cells than the list holds -- that plan splits none
+        sky = E.camera(W, H, 1, 1, facing=(0.0, 1.0, 0.0))
+        drag = E.camera(W, H, 1, 1)
+        eng.set_tuning(frame_plan=0)
+        want_sky, want_drag = run(eng, sky, variant=variant), run(eng, drag, variant=variant)
+        eng.set_tuning(frame_plan=1)
+        for cam, want in ((sky, want_sky), (drag, want_drag), (drag, want_drag), (sky, want_sky), (drag, want_drag)):
+            got = run(eng, cam, variant=variant)
+            for k in ("fb", "face", "t", "casts"):
+                assert np.array_equal(np.asarray(want[k]).view(np.uint32), np.asarray(got[k]).view(np.uint32)), k
+    finally:
+        eng.set_tuning(**base)
 
 
 def test_renderer_api_start_wait(eng):
@@ -446,3 +492,34 @@ def test_gpu_work_counters_equal_reference_work(eng, name, variant):
         assert 0 < c["n_tri"] <= g["counters"]["n_tri"], (c["n_tri"], g["counters"]["n_tri"])
     else:
         assert c["n_tri"] == g["counters"]["n_tri"], (c["n_tri"], g["counters"]["n_tri"])
+
+
+def test_bgr_exchange_reassembles_frames(eng):
+    """The multi-GPU 3-byte exchange on one GPU: 3 ranks' packed shard frames (2 frames per
+    launch) packed by atr_pack_bgr into one byte buffer laid out as rank 0 receives it
+    (shard.frame_offsets), expanded and scattered by atr_scatter_bgr through the assembly index:
+    every frame equals the full-frame render, and the bytes equal the host reference."""
+    from atray_amd import shard as S
+    upload(eng, "Dragon", True)
+    W, H, F, world = 480, 270, 2, 3
+    cams = [E.camera(W, H, 1, 1, eye=(0.1 + 0.05 * f, 2.0, 0.0)) for f in range(F)]
+    plan = S.ShardPlan(W, H, world, 64)
+    off = S.frame_offsets(plan, F)
+    big = torch.zeros(3 * F * W * H, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for r in range(world):
+        n = plan.sizes[r]
+        fb = torch.zeros(F * n, dtype=torch.int32, device="cuda")
+        fr = E.atr_frame(E.ATR_LAYOUT_PACKED, fb.data_ptr(), None, None, None, None, None)
+        eng.render_start_cameras(cams, plan.tiles[r], fr, n, SEED, stream=s)
+        eng.pack_bgr(fb.data_ptr(), F * n, big[3 * off[r]:].data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        want = S.pack_bgr_host(fb.cpu().numpy().view(np.uint32))
+        assert np.array_equal(big[3 * off[r]:3 * off[r] + 3 * F * n].cpu().numpy(), want)
+    dst = torch.from_numpy(S.frames_assembly_index(plan, F)).cuda()
+    img = torch.zeros(F * W * H, dtype=torch.int32, device="cuda")
+    eng.scatter_bgr(big.data_ptr(), F * W * H, dst.data_ptr(), img.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    for f in range(F):
+        full = run(eng, cams[f])
+        assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])

@@ -154,3 +154,20 @@ def test_two_rank_pipelined_gather_reassembles_every_frame(tmp_path):
     assert len(frames) == 5
     for k in range(5):
         assert np.array_equal(frames[k], face.astype(np.int64) + k)
+
+
+def test_bgr_pack_scatter_host_roundtrip():
+    """The 3-byte exchange's host references (atr_pack_bgr / atr_scatter_bgr): BGRX pixels survive
+    pack -> scatter through an assembly permutation, and a nonzero X byte is refused."""
+    from atray_amd.shard import pack_bgr_host, scatter_bgr_host
+    rng = np.random.default_rng(1)
+    fb = rng.integers(0, 1 << 24, size=1000, dtype=np.uint32)
+    p = pack_bgr_host(fb)
+    assert p.dtype == np.uint8 and p.size == 3000
+    assert list(p[:3]) == [fb[0] & 255, (fb[0] >> 8) & 255, (fb[0] >> 16) & 255]
+    perm = rng.permutation(1000)
+    img = np.zeros(1000, np.uint32)
+    scatter_bgr_host(p, perm, img)
+    assert np.array_equal(img[perm], fb)
+    with pytest.raises(AssertionError):
+        pack_bgr_host(np.array([1 << 24], np.uint32))
