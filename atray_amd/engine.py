@@ -111,6 +111,7 @@ EXPORTS = [
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_render_phase_clocks", "atr_render_path_counters", "atr_default_tuning", "atr_set_tuning",
     "atr_get_tuning", "atr_render_simd_counters", "atr_pack_bgr", "atr_scatter_bgr",
+    "atr_render_plan_info",
 ]
 
 _lib = None
