@@ -764,12 +764,15 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 
 // ------------------------------------------------------------------ get_intersection_data
 enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5,
-       SCHED_FLAT = 6, SCHED_HYBRID = 7, SCHED_FLAT_NOCC = 9, SCHED_HYBRID_NOCC = 10, SCHED_FLAT_UT = 11 };
+       SCHED_FLAT = 6, SCHED_HYBRID = 7, SCHED_FLAT_NOCC = 9, SCHED_HYBRID_NOCC = 10, SCHED_FLAT_UT = 11,
+       SCHED_FLAT_REGEN = 12 };
 // The FLAT / HYBRID family (wave-wide leaf steps, LDS path stash). FLAT and HYBRID compact the full
 // tests' candidates over the wavefront (cand_rounds); the _NOCC schedules are the round-2 kernels
 // that test a cluster's candidates in its lane (diagnostic); FLAT_UT walks every
 // bounce's DFS passes wave-wide (diagnostic).
-constexpr bool sched_flat(int sc) { return sc == SCHED_FLAT || sc == SCHED_FLAT_NOCC || sc == SCHED_FLAT_UT; }
+constexpr bool sched_flat(int sc) {
+    return sc == SCHED_FLAT || sc == SCHED_FLAT_NOCC || sc == SCHED_FLAT_UT || sc == SCHED_FLAT_REGEN;
+}
 constexpr bool sched_hyb(int sc) { return sc == SCHED_HYBRID || sc == SCHED_HYBRID_NOCC; }
 constexpr bool sched_cc(int sc) { return sc != SCHED_FLAT_NOCC && sc != SCHED_HYBRID_NOCC; }
 constexpr int sched_waves(int sc) { return sc == SCHED_TILE8 ? 8 : 4; }
@@ -797,7 +800,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                 // the camera rays of a bounce loop (one origin, coherent) take HYBRID's primary flavour
                 if (first)
                     tree_closest_flat<COUNT, true, true, false, true, true, false, CC>(r, m, active, h, err, ct, hyb_a, hyb_b);
-                else if constexpr (SCHED == SCHED_FLAT)  // LDS leaf buffer: fewer VGPRs, 5 waves/SIMD (§4d)
+                else if constexpr (SCHED == SCHED_FLAT || SCHED == SCHED_FLAT_REGEN)  // LDS leaf buffer: fewer VGPRs, 5 waves/SIMD (§4d)
                     tree_closest_flat<COUNT, false, true, true, false, false, false, true>(r, m, active, h, err, ct);
                 else if constexpr (SCHED == SCHED_FLAT_UT)
                     tree_closest_flat<COUNT, false, true, true, false, true, false, CC>(r, m, active, h, err, ct);
@@ -936,6 +939,113 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
     return ret;
 }
 
+// FLAT_REGEN: the pixel loop of a multi-bounce render (renderer.cpp:336-357 around cast_ray
+// :213-262) with path regeneration. In cast_ray's loop a lane whose path has ended (sky, or the
+// bounce limit) idles until the wavefront's longest path of that sample is done; on Dragon C4 a
+// path traces 1.5 rays on average and the wave's slowest lane up to 5. Here every lane runs its
+// own (sample, bounce) sequence: a lane whose path ends adds the sample's colour and starts its
+// next sample's camera ray in the same step, so each wave step traces a ray in every lane that
+// still has samples left. A pixel's samples, its bounces and its PCG draws happen in the
+// reference's order (AA jitter x then y at a sample's start, three rand_bi per non-sky hit), and
+// the colour sums in sample order, so every output equals cast_ray's bit for bit. A step whose
+// tracing lanes all hold camera rays (one origin: the first step, and whenever the lanes'
+// samples line up) takes HYBRID's primary flavour; every other step FLAT's dealt rounds. The path
+// state waits in private memory during the query, as in FLAT.
+constexpr int kRegenStash = 20;
+template <int SCHED, bool COUNT>
+__device__ __forceinline__ V3 pixel_paths_regen(const DScene* __restrict__ S, uint32_t spp, int32_t bl, bool aa,
+                                                float hpw, float hph, V3 eye, V3 fc, V3 cx, V3 cy, float film_x,
+                                                float film_y, bool active, uint64_t& st, uint64_t stream,
+                                                uint32_t& casts, uint32_t& traced, uint32_t& hit_face, float& hit_t,
+                                                int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
+    // the camera's fields arrive by value (uniform: SGPRs); a reference into the kernel argument's
+    // per-frame camera array made the compiler copy the whole argument to private memory
+    volatile uint32_t L[kRegenStash];
+    V3 col = mk(0.f, 0.f, 0.f), ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
+    uint32_t smp = 0;
+    int32_t i = 0;
+    bool have = active && spp > 0 && bl > 0;
+    V3 o = eye, d = mk(0.f, 0.f, 1.f);
+    // sample smp's camera ray (:338-351): jittered per sample with AA, else the pixel centre's
+    auto camera_ray = [&]() {
+        if (aa) {
+            const float xo = rand_bi(st, stream) * hpw + film_x;
+            const float yo = rand_bi(st, stream) * hph + film_y;
+            d = unit(sub(add(add(fc, scale(cx, xo)), scale(cy, yo)), eye));
+        } else {
+            d = unit(sub(add(add(fc, scale(cx, film_x)), scale(cy, film_y)), eye));
+        }
+    };
+    if (have) camera_ray();
+    for (;;) {
+        if (__ballot(have) == 0) break;
+        // every tracing lane holds a camera ray: one origin (inactive lanes keep o = eye too)
+        const bool first = __ballot(have && i != 0) == 0;
+        if constexpr (COUNT) {
+            const int bk = i < 2 ? i : 2;
+            ct.steps[first ? 0 : 1] += (threadIdx.x & 63) == 0 ? 1u : 0u;
+            ct.active[bk] += have ? 1u : 0u;
+        }
+        L[0] = __float_as_uint(ret.x); L[1] = __float_as_uint(ret.y); L[2] = __float_as_uint(ret.z);
+        L[3] = __float_as_uint(w.x); L[4] = __float_as_uint(w.y); L[5] = __float_as_uint(w.z);
+        L[6] = __float_as_uint(col.x); L[7] = __float_as_uint(col.y); L[8] = __float_as_uint(col.z);
+        L[9] = uint32_t(st); L[10] = uint32_t(st >> 32);
+        L[11] = casts; L[12] = traced; L[13] = hit_face; L[14] = __float_as_uint(hit_t);
+        L[15] = smp; L[16] = uint32_t(i); L[17] = have ? 1u : 0u;
+        L[18] = __float_as_uint(film_x); L[19] = __float_as_uint(film_y);
+        Isect id;
+        id.type = T_NONE;
+        intersect_scene<SCHED, COUNT>(S, o, d, have, id, err, ct, hyb_a, hyb_b, first);
+        auto gf = [&](int k) { return __uint_as_float(L[k]); };
+        ret = mk(gf(0), gf(1), gf(2));
+        w = mk(gf(3), gf(4), gf(5));
+        col = mk(gf(6), gf(7), gf(8));
+        st = uint64_t(L[9]) | (uint64_t(L[10]) << 32);
+        casts = L[11]; traced = L[12]; hit_face = L[13]; hit_t = gf(14);
+        smp = L[15]; i = int32_t(L[16]); have = L[17] != 0;
+        film_x = gf(18); film_y = gf(19);
+        if (!have) continue;
+        ++traced;
+        if (smp == 0 && i == 0) { hit_face = id.face; hit_t = id.t; }  // sample 0's camera ray
+        const DMaterial& mat = S->mats[id.material];
+        const V3 emission = mk(mat.ex, mat.ey, mat.ez);
+        bool end;
+        if (id.type == T_SKY) {  // :225-229
+            ret = add(ret, had(w, emission));
+            casts += uint32_t(i);
+            end = true;
+        } else {  // :231-258
+            float att = dot(neg(d), id.normal);
+            V3 n = id.normal;
+            if (att < 0) { n = neg(n); att = 0; }
+            V3 pure = sub(d, scale(n, (2 * dot(d, n))));
+            pure = unit(pure);
+            const float r0 = rand_bi(st, stream);
+            const float r1 = rand_bi(st, stream);
+            const float r2 = rand_bi(st, stream);
+            V3 rnd = add(mk(r0, r1, r2), n);
+            rnd = unit(rnd);
+            o = add(o, scale(d, id.t));
+            d = unit(lerp3(rnd, pure, mat.scatter));
+            ret = add(ret, had(w, emission));
+            w = had(w, scale(mk(mat.rx, mat.ry, mat.rz), att));
+            ++i;
+            end = i >= bl;
+            if (end) casts += uint32_t(bl);  // :260, the path ran to the bounce limit
+        }
+        if (end) {  // the sample's colour (:353-356), then the next sample's camera ray
+            col = add(col, ret);
+            ret = mk(0.f, 0.f, 0.f);
+            w = mk(1.f, 1.f, 1.f);
+            o = eye;
+            i = 0;
+            if (++smp < spp) camera_ray();
+            else have = false;
+        }
+    }
+    return col;
+}
+
 __device__ __forceinline__ int remap_xcd(int wg, int nwg, int chunk) {
     const int x = wg % 8;  // the hardware deals workgroups round-robin over the 8 XCDs
     if (chunk > 0) {
@@ -1018,6 +1128,14 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
                 ++traced;
             }
         }
+    } else if constexpr (SCHED == SCHED_FLAT_REGEN) {
+        col = pixel_paths_regen<SCHED, COUNT>(
+            S, __builtin_amdgcn_readfirstlane(cm.samples_per_pixel), __builtin_amdgcn_readfirstlane(cm.bounce_limit),
+            __builtin_amdgcn_readfirstlane(cm.anti_aliasing) != 0,
+            __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, cm.half_pixel_width))),
+            __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, cm.half_pixel_height))),
+            eye, fc, cx, cy, film_x, film_y, active, st, stream, casts, traced, hit_face, hit_t, err, ct, P.hyb_a,
+            P.hyb_b);
     } else
     for (uint32_t s = 0; s < cm.samples_per_pixel; ++s) {
         if (cm.anti_aliasing) {  // :338-343
@@ -1138,6 +1256,8 @@ ATR_INST4(SCHED_LANE) ATR_INST4(SCHED_WAVE) ATR_INST4(SCHED_TILE4) ATR_INST4(SCH
 ATR_INST4(SCHED_FLAT) ATR_INST4(SCHED_HYBRID)
 ATR_INST(SCHED_FLAT_NOCC, false, false) ATR_INST(SCHED_FLAT_NOCC, true, false)
 ATR_INST(SCHED_FLAT_UT, false, false) ATR_INST(SCHED_FLAT_UT, true, false)
+ATR_INST4(SCHED_FLAT_REGEN)
+template __global__ void render_kernel<SCHED_FLAT_REGEN, false, false, 5>(RenderParams);
 ATR_INST(SCHED_HYBRID_NOCC, true, true) ATR_INST(SCHED_HYBRID_NOCC, true, false)
 ATR_INST(SCHED_HYBRID_NOCC, false, false)
 
@@ -1268,6 +1388,10 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
             if (prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_HYBRID_NOCC, false, true, 6>), g, b, 0, s, P);
             else if (count) { if (prim) launch_one<atr::SCHED_HYBRID_NOCC, true, true>(P, s); else launch_one<atr::SCHED_HYBRID_NOCC, true, false>(P, s); }
             else launch_one<atr::SCHED_HYBRID_NOCC, false, false>(P, s);
+        } else if (sched == 101 || sched == 102) {  // FLAT with path regeneration (102: 5 waves/SIMD)
+            if (sched == 102 && !prim && !count)
+                hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT_REGEN, false, false, 5>), g, b, 0, s, P);
+            else launch_sched<atr::SCHED_FLAT_REGEN>(P, count, prim, s);
         } else if (sched == 100) {
             if (prim) return hipErrorInvalidValue;
             if (count) launch_one<atr::SCHED_FLAT_UT, true, false>(P, s);

@@ -716,6 +716,20 @@ def run(args):
         assert rc == 0
         return float(np.mean([a.elapsed_time(b) for a, b in evs]))
     kern_ms = time_one(roof_variant)
+
+    def latency_one(v, n=10):
+        # the live view's case: one frame on an idle GPU, render start -> framebuffer complete
+        # (atr_last_kernel_ms: the library's events around the render alone; the plan kernels that
+        # prepare the NEXT frame's dispatch run after that point and are in time_one's period)
+        lat = []
+        for _ in range(n):
+            eng.render_start(app_cam, tiles, frame_of(0), SEED, stream=s0.cuda_stream, variant=v)
+            torch.cuda.synchronize()
+            lat.append(eng.last_kernel_ms())
+        rc, _ = eng.wait()
+        assert rc == 0
+        return float(np.median(lat))
+    lat_ms = latency_one(roof_variant)
     # steady state (informational, not `value`): 64 further orbit frames in 16-frame launches on the
     # same streams, after the timed region -- the rate without a short run's pipeline fill and drain
     steady = None
@@ -771,6 +785,7 @@ def run(args):
             out["check_mismatched_pixels"] = check
         n1 = live_ctr["n_rays"]
         out["single_frame"] = {"kernel_ms": round(kern_ms, 4), "mrays_s": round(n1 / kern_ms / 1e3, 1),
+                               "latency_ms": round(lat_ms, 4),
                                "camera": "app", "rays": n1, "variant": VARIANT_NAMES.get(roof_variant, roof_variant)}
         # roofline. HBM: the bytes HBM actually moved (PMC, per timed launch of this
         # command's shape, per frame) over the measured time per frame -- the kernel's real HBM

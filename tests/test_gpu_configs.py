@@ -9,6 +9,8 @@ schedules must agree with each other (LANE: the reference's exact per-triangle w
 multi-bounce default; CLUSTER: the primary-ray default; PERSIST: persistent lanes), a
 size-independent property.
 Needs an MI355X (-m gpu)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -21,6 +23,8 @@ from tests.goldens import SEED  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 RGB_RTOL = 1e-5
+# ATR_TEST_EXTRA_VARIANTS=a,b,...: diagnostic schedule codes added to the full-size lists
+EXTRA = [int(v) for v in os.environ.get("ATR_TEST_EXTRA_VARIANTS", "").split(",") if v]
 
 
 @pytest.fixture(scope="module")
@@ -98,7 +102,7 @@ C5_BANDS = [(1112, 1114), (626, 627)]
 
 
 @pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
-                                     E.ATR_KERNEL_HYBRID])
+                                     E.ATR_KERNEL_HYBRID] + EXTRA)
 def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
     """C4 through AUTO (= FLAT for multi-bounce, capi.cpp auto_sched), CLUSTER, PERSIST and HYBRID."""
     o = render(eng, E.camera(1920, 1080, 64, 5), variant)
@@ -134,7 +138,7 @@ ORBIT = [(0.1 + 0.5 * np.sin(a), 2.0, 0.5 * (1 - np.cos(a))) for a in np.linspac
 
 
 @pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
-                                     E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID])
+                                     E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID] + EXTRA)
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (2, 3)])
 @pytest.mark.parametrize("layout", [E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED])
 def test_per_frame_cameras_equal_single_renders(eng, variant, spp, bounces, layout):

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 3 measurement set for the multi-bounce configs: c4/c5 bench lines, c4 PMC groups
+# (FLAT, 64 spp x 5 bounces, one frame per launch), then the 8-way shard simulation.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r3m
+mkdir -p $O
+timeout -k 10 300 python3 bench.py --config c4 --steps 8 --warmup 1 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err || { tail -20 $O/bench_c4.err; exit 1; }
+tail -c 300 $O/bench_c4.json; echo
+OUT_DIR=r3m/pmc_c4 PMC_SPP=64 PMC_BOUNCES=5 bash tools/gpu_pmc2.sh || exit $?
+timeout -k 10 300 python3 bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || { tail -20 $O/bench_c5.err; exit 1; }
+tail -c 300 $O/bench_c5.json; echo
+bash tools/gpu_r3_sim8.sh
