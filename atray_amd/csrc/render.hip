@@ -1268,6 +1268,7 @@ template __global__ void render_kernel<SCHED_HYBRID, false, true, 7>(RenderParam
 template __global__ void render_kernel<SCHED_HYBRID, false, false, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, false, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_FLAT, false, false, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT, false, false, 7>(RenderParams);
 #undef ATR_INST4
 #undef ATR_INST
 template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
@@ -1410,9 +1411,10 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
         else launch_sched<atr::SCHED_HYBRID>(P, count, prim, s);
         return hipGetLastError();
     }
-    if (sched >= 64) {  // FLAT bounce loops at 64 + n waves/SIMD (diagnostic: 4, 5, 6)
+    if (sched >= 64) {  // FLAT bounce loops at 64 + n waves/SIMD (diagnostic: 4, 5, 6, 7)
         const int o = sched - 64;
-        if (!count && o == 6 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 6>), g, b, 0, s, P);
+        if (!count && o == 7 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 7>), g, b, 0, s, P);
+        else if (!count && o == 6 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 6>), g, b, 0, s, P);
         else if (!count && o == 5 && !prim) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
         else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
         return hipGetLastError();
@@ -1444,9 +1446,13 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
     }
     switch (sched) {
         case 1: launch_sched<atr::SCHED_WAVE>(P, count, prim, s); break;
-        case 6:  // bounce loops at 5 waves/SIMD (the LDS leaf buffer and private path stash let them fit:
-                 // 22.5 KB LDS, <= 102 VGPRs)
-            if (!prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 5>), g, b, 0, s, P);
+        case 6:  // bounce loops: one frame at 6 waves/SIMD (80 VGPRs; its slowest cells set the latency),
+                 // frames in flight at 7 (72 VGPRs, the LDS limit: 7 x 22.5 KB per CU). The
+                 // spills (54 / 83 dwords) cost less than the latency the extra waves hide: c4 1,376 ->
+                 // 1,536 (6) -> 1,630 (7) Mrays/s
+            if (!prim && !count && P.frame_blocks > 0)
+                hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 7>), g, b, 0, s, P);
+            else if (!prim && !count) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT, false, false, 6>), g, b, 0, s, P);
             else launch_sched<atr::SCHED_FLAT>(P, count, prim, s);
             break;
         case 7:  // primaries: one frame at 6 waves/SIMD (its slowest cells set the latency), frames in

@@ -6,6 +6,9 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r3sim
 mkdir -p $O
+( while sleep 30; do date +%s >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB" EXIT
 run() {  # name, timeout, args
   timeout -k 10 $2 python3 bench.py --no-pmc --no-cpu-baseline --no-prep --no-steady "${@:3}" > $O/$1.json 2> $O/$1.err || { tail -5 $O/$1.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/$1.json').read().strip().splitlines()[-1]); print('$1', d['value'], d['ms_per_step'], d['single_frame']['kernel_ms'], d['config']['shard_pixels'][:1] if 'sim' not in d else d['sim'])"
