@@ -506,8 +506,9 @@ int auto_sched(int32_t variant, const atr_camera& cam) {
 hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s);
 int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStream_t s) {
     const int32_t nb = int32_t(bs->host.size());
-    const bool user_plan = !c->cplan.empty() && c->cplan_w == bs->width && c->cplan_h == bs->height;
-    const bool use = c->tune.frame_plan && !user_plan && nb > 0 && sched != kSchedPersist &&
+    // on top of a user cell plan too: its classes order the base list (and the multi-frame
+    // launches), the frame plan re-orders that list for single frames by their measured cost
+    const bool use = c->tune.frame_plan && nb > 0 && sched != kSchedPersist &&
                      (!bs->plan_ready || bs->plan_stream == s);
     if (!use) {
         HIPCHK(launch_render(c, P, sched, s));

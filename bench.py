@@ -267,6 +267,9 @@ def main():
     ap.add_argument("--cell-split", default="",
                     help="P:FRAC -- the FRAC most expensive 8x8 cells (measured on the calibration frames) are "
                          "traced by P waves each (atr_set_cell_plan; scheduling only, same outputs)")
+    ap.add_argument("--cell-order", default="graded", choices=["list", "graded"],
+                    help="graded (default): cells dispatched by the calibration frames' measured cost, heaviest "
+                         "class first (atr_set_cell_plan classes); list: tile list order (Morton within a tile)")
     ap.add_argument("--stream-priority", type=int, default=-1,
                     help="1: stream 0 at the device's highest priority (its launch completes first, so at N > 1 "
                          "its exchange overlaps the other launches' rendering); -1 (default) = on for N > 1")
@@ -468,16 +471,33 @@ def run(args):
         plan = S.ShardPlan(W, H, pw, args.side)
     sizes = plan.sizes
     cell_split = None
-    if args.cell_split:  # the heaviest cells of the run's calibration frames, split over P waves
-        parts, frac = args.cell_split.split(":")
+    if args.cell_split or args.cell_order != "list":
+        # the run's calibration frames' per-cell costs: the heaviest cells split over P waves
+        # (--cell-split P:FRAC) and/or every cell graded into dispatch classes by cost, heaviest
+        # first (--cell-order graded: the single-frame plan's class fractions, plan.hip), so a
+        # launch's slowest cells start first instead of forming its tail
         ks = calib_frames(args)
-        cc = sum(eng.cell_costs(cams[k % n_orbit], SEED, variant) for k in ks)
-        nsplit = int(round(float(frac) * cc.size))
+        cc = sum(eng.cell_costs(cams[k % n_orbit], SEED, variant) for k in ks).ravel()
         cplan = np.zeros(cc.size, np.uint8)
-        if nsplit > 0:
-            cplan[np.argsort(-cc.ravel(), kind="stable")[:nsplit]] = int(parts)
+        corder = np.argsort(-cc, kind="stable")
+        cell_split = {"of": int(cc.size)}
+        if args.cell_split:
+            parts, frac = args.cell_split.split(":")
+            nsplit = int(round(float(frac) * cc.size))
+            cplan[corder[:nsplit]] = int(parts)
+            cell_split.update(parts=int(parts), cells=nsplit)
+        if args.cell_order != "list":
+            live = int((cc > 0).sum())
+            bounds = [0.02, 0.05, 0.10, 0.20, 0.30, 0.50, 0.75]  # cumulative, heaviest first
+            cls = np.zeros(cc.size, np.uint8)
+            crank = np.empty(cc.size, np.int64)
+            crank[corder] = np.arange(cc.size)
+            for k, f in enumerate(bounds):  # class 7 for the top 2 %, ..., 0 for the rest
+                cls[crank >= int(round(f * live))] = 6 - k
+            cls[crank < int(round(bounds[0] * live))] = 7
+            cplan |= (cls << 4).astype(np.uint8)
+            cell_split["order"] = args.cell_order
         eng.set_cell_plan(W, H, cplan)
-        cell_split = {"parts": int(parts), "cells": nsplit, "of": int(cc.size)}
     if pw > 1 or args.single_tiles == "cost":
         tiles = E.tiles_array(plan.tiles[pr])
     else:
@@ -773,13 +793,14 @@ def run(args):
                           **({"exchange": "bgr (3 B/px)" if bgr else "bgrx (4 B/px)"} if pw > 1 else {}),
                           "launches": launch_sizes(args.steps, F_, S_),
                           "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),
-                          "cell_split": cell_split,
+                          "cell_plan": cell_split,
                           "shard_pixels": [int(x) for x in sizes]},
                **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange"}} if sim else {}),
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
         if steady:
             out["steady_state"] = steady
-        if (pw > 1 and args.plan == "cost") or args.cell_split or (pw == 1 and args.single_tiles == "cost"):
+        if (pw > 1 and args.plan == "cost") or args.cell_split or args.cell_order != "list" or \
+            (pw == 1 and args.single_tiles == "cost"):
             out["config"]["calibration_frames"] = calib_frames(args)  # orbit positions, all before the timed ones
         if check is not None:
             out["check_mismatched_pixels"] = check

@@ -169,8 +169,9 @@ typedef struct {
     int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
                                dispatches its tiles' cells by that launch's measured cost, heaviest
                                first, the heaviest 1 % over two waves (built on the GPU after each
-                               such launch); 0: list order; default 1. Ignored while
-                               an atr_set_cell_plan plan is set for the image size */
+                               such launch); 0: list order; default 1. With an
+                               atr_set_cell_plan plan for the image size it re-orders that plan's
+                               block list */
     int32_t reserved[5];    /* must be 0 */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
