@@ -103,8 +103,11 @@ __device__ __forceinline__ bool cluster_pads(const Ray& r, const ScreenRay& sr, 
     const float fx = fmaxf(fabsf(lo.x - r.o.x), fabsf(hi.x - r.o.x));
     const float fy = fmaxf(fabsf(lo.y - r.o.y), fabsf(hi.y - r.o.y));
     const float fz = fmaxf(fabsf(lo.z - r.o.z), fabsf(hi.z - r.o.z));
-    // W >= |o - a| + |edge| for every primitive inside (far corner; L1 extent >= diagonal)
-    const float W = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0000005f + (ex + ey + ez);
+    // W >= |o - a| + |edge| for every primitive inside (far corner; L1 extent >= diagonal). The
+    // hardware square root (v_sqrt_f32, within 1 ulp) instead of the correctly rounded expansion
+    // (~15 VALU: denormal scaling, two FMA corrections): W only has to bound the distance from
+    // above, the 1 + 2^-21 factor covers 8 ulp, and the 2^-63 term the flushed denormal case
+    const float W = (__builtin_amdgcn_sqrtf(fx * fx + fy * fy + fz * fz) + 1.0842022e-19f) * 1.0000005f + (ex + ey + ez);
     const float P = lo.w;  // >= |ab||ac| of every primitive inside
     const float gl = W * (P * (kPadRel / (0.9f * kTol)) + kPadAbs);
     const float gt = W * (P * (kPadRel / (0.9f * kTau)) + kPadAbs);
@@ -136,17 +139,21 @@ __device__ __forceinline__ bool cluster_pads(const Ray& r, const ScreenRay& sr, 
 
 // Screen of 8 primitives g .. g + 7 of n: words a0, a1 hold (nx, ny) of slots g .. g + 7 as f16,
 // z the nz of slots g .. g + 7 (two per word). Bit j: slot g + j needs the full test.
+// (The slots past n are masked off once per cluster by the caller, not per primitive.)
 __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float dlo, float dhi, uint4_t a0, uint4_t a1,
-                                            uint4_t z, uint32_t g, uint32_t n) {
+                                            uint4_t z) {
     const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
     uint32_t gc = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const h2_t pxy = __builtin_bit_cast(h2_t, xy[j]), pz = __builtin_bit_cast(h2_t, zz[j / 2]);
-        const float dz = __builtin_amdgcn_fdot2((j & 1) ? sr.dz_hi : sr.dz_lo, pz, 0.0f, false);
+        // the z term with a zero accumulator operand (VOP3P v_dot2_f32_f16 ..., 0): the builtin
+        // selects v_dot2c_f32_f16, whose accumulator is its destination, plus a v_mov of the zero
+        float dz;
+        asm("v_dot2_f32_f16 %0, %1, %2, 0" : "=v"(dz) : "v"((j & 1) ? sr.dz_hi : sr.dz_lo), "v"(pz));
         const float e = __builtin_amdgcn_fdot2(sr.dxy, pxy, dz, false) * nq;
-        if (g + j < n && e >= dlo && e < dhi) gc |= 1u << j;
+        if (e >= dlo && e < dhi) gc |= 1u << j;
     }
     return gc;
 }
@@ -170,8 +177,8 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
     const float nq = -hi.w;
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
-        cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8], g, n) << g;
-    return cand;
+        cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8]) << g;
+    return cand & ((2u << (n - 1)) - 1u);  // slots [0, n), 1 <= n <= 16
 }
 
 // Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and
