@@ -780,6 +780,38 @@ constexpr bool sched_coop(int sc) {  // lanes must stay in lockstep loops (workg
     return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && !sched_flat(sc) && !sched_hyb(sc);
 }
 
+// A model's table pointers as wave-uniform GLOBAL pointers: read once per query into SGPRs
+// (readfirstlane) and cast to the global address space. Through the DScene reference the compiler
+// re-loaded each pointer with a vector load before every use (a dependent round trip in front of
+// every cluster record, candidate and leaf range) and, the pointers being generic, issued the
+// table loads as flat loads.
+template <class T>
+__device__ __forceinline__ T* uniform_global(T* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v)), hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    using G = __attribute__((address_space(1))) T;
+    return (T*)(reinterpret_cast<G*>((uint64_t(hi) << 32) | lo));
+}
+__device__ __forceinline__ DModel uniform_model(const DModel& src) {
+    DModel m = src;
+    m.nodes = uniform_global(m.nodes);
+    m.inner = uniform_global(m.inner);
+    m.leaf_range = uniform_global(m.leaf_range);
+    m.tris = uniform_global(m.tris);
+    m.t0 = uniform_global(m.t0);
+    m.t1 = uniform_global(m.t1);
+    m.t2 = uniform_global(m.t2);
+    m.tface = uniform_global(m.tface);
+    m.clus = uniform_global(m.clus);
+    m.cl_range = uniform_global(m.cl_range);
+    m.cnrm = uniform_global(m.cnrm);
+    m.c0 = uniform_global(m.c0);
+    m.c1 = uniform_global(m.c1);
+    m.c2 = uniform_global(m.c2);
+    m.cface = uniform_global(m.cface);
+    return m;
+}
+
 template <int SCHED, bool COUNT, bool PR = false>
 __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active,
                                                 Isect& id, int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b,
@@ -791,7 +823,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
     float fu = 0.f, fv = 0.f;
     const int32_t nmodels = __builtin_amdgcn_readfirstlane(S->nmodels);  // uniform: an SGPR, not a VGPR
     for (int32_t i = 0; i < nmodels; ++i) {
-        const DModel& m = S->models[i];
+        const DModel m = uniform_model(S->models[i]);
         if (m.has_tree) {  // USE_KD_TREE (:49-57)
             Hit h;
             if constexpr (SCHED == SCHED_WAVE) tree_closest_wave<COUNT>(r, m, active, h, err, ct);
