@@ -780,18 +780,11 @@ constexpr bool sched_coop(int sc) {  // lanes must stay in lockstep loops (workg
     return sc != SCHED_LANE && sc != SCHED_CLUSTER && sc != SCHED_CLUSTER_K4 && !sched_flat(sc) && !sched_hyb(sc);
 }
 
-// A model's table pointers as wave-uniform GLOBAL pointers: read once per query into SGPRs
-// (readfirstlane) and cast to the global address space. Through the DScene reference the compiler
+// A model's table pointers as wave-uniform GLOBAL pointers (uniform_global, trace.h): read once per
+// query into SGPRs and cast to the global address space. Through the DScene reference the compiler
 // re-loaded each pointer with a vector load before every use (a dependent round trip in front of
 // every cluster record, candidate and leaf range) and, the pointers being generic, issued the
 // table loads as flat loads.
-template <class T>
-__device__ __forceinline__ T* uniform_global(T* p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v)), hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
-    using G = __attribute__((address_space(1))) T;
-    return (T*)(reinterpret_cast<G*>((uint64_t(hi) << 32) | lo));
-}
 __device__ __forceinline__ DModel uniform_model(const DModel& src) {
     DModel m = src;
     m.nodes = uniform_global(m.nodes);
@@ -881,10 +874,6 @@ constexpr int kStash = 16;
 // The stash lives in LDS (a lane-private column, stride 64 words) or, for FLAT, in the lane's
 // private (scratch) memory: a volatile local array, which the compiler must keep in memory (stride
 // 1), so the kernel's LDS is only the scan's 22.5 KB and more workgroups fit a CU.
-template <int ST, class PT>
-__device__ __forceinline__ void stash_put(PT* L, int k, uint32_t v) { L[ST * k] = v; }
-template <int ST, class PT>
-__device__ __forceinline__ uint32_t stash_get(PT* L, int k) { return L[ST * k]; }
 
 template <int SCHED, bool COUNT>
 __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d, int32_t bounce_limit,
@@ -893,13 +882,16 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
                                        int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b, V3& acc) {
     constexpr bool STASH = sched_flat(SCHED) || sched_hyb(SCHED);
     constexpr bool PRIV = SCHED == SCHED_FLAT;  // the stash in private memory (above)
-    constexpr int ST = PRIV ? 1 : 64;
     __shared__ uint32_t s_stash[STASH && !PRIV ? 4 : 1][PRIV ? 1 : kStash][64];
-    volatile uint32_t pstash[PRIV ? kStash : 1];
-    using PT = std::conditional_t<PRIV, volatile uint32_t, uint32_t>;
-    PT* L;
-    if constexpr (PRIV) L = pstash;
-    else L = &s_stash[STASH ? threadIdx.x >> 6 : 0][0][threadIdx.x & 63];
+    // the private stash is indexed directly (scratch loads and stores); through a generic pointer
+    // every access was a flat load or store
+    // (not volatile: volatile private accesses are left generic, i.e. flat loads and stores; the
+    // array's address escapes into empty asm statements around the query instead, which keeps
+    // its values in memory through the query)
+    uint32_t pstash[PRIV ? kStash : 1];
+    uint32_t* const L = &s_stash[STASH ? threadIdx.x >> 6 : 0][0][threadIdx.x & 63];
+#define stash_put(k, v) do { if constexpr (PRIV) pstash[k] = (v); else L[64 * (k)] = (v); } while (0)
+#define stash_get(k) (PRIV ? pstash[(PRIV ? (k) : 0)] : L[64 * (k)])
     V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
     int32_t i = 0;
     bool live = active;
@@ -920,27 +912,32 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
         Isect id;
         id.type = T_NONE;
         if constexpr (STASH) {
-            stash_put<ST>(L, 0, __float_as_uint(ret.x)); stash_put<ST>(L, 1, __float_as_uint(ret.y));
-            stash_put<ST>(L, 2, __float_as_uint(ret.z)); stash_put<ST>(L, 3, __float_as_uint(w.x));
-            stash_put<ST>(L, 4, __float_as_uint(w.y)); stash_put<ST>(L, 5, __float_as_uint(w.z));
-            stash_put<ST>(L, 6, __float_as_uint(acc.x)); stash_put<ST>(L, 7, __float_as_uint(acc.y));
-            stash_put<ST>(L, 8, __float_as_uint(acc.z));
-            stash_put<ST>(L, 9, uint32_t(st)); stash_put<ST>(L, 10, uint32_t(st >> 32));
-            stash_put<ST>(L, 11, casts); stash_put<ST>(L, 12, traced); stash_put<ST>(L, 13, hit_face);
-            stash_put<ST>(L, 14, __float_as_uint(hit_t));
-            __asm__ volatile("" ::: "memory");  // the values below come back from LDS
+            stash_put(0, __float_as_uint(ret.x)); stash_put(1, __float_as_uint(ret.y));
+            stash_put(2, __float_as_uint(ret.z)); stash_put(3, __float_as_uint(w.x));
+            stash_put(4, __float_as_uint(w.y)); stash_put(5, __float_as_uint(w.z));
+            stash_put(6, __float_as_uint(acc.x)); stash_put(7, __float_as_uint(acc.y));
+            stash_put(8, __float_as_uint(acc.z));
+            stash_put(9, uint32_t(st)); stash_put(10, uint32_t(st >> 32));
+            stash_put(11, casts); stash_put(12, traced); stash_put(13, hit_face);
+            stash_put(14, __float_as_uint(hit_t));
+            if constexpr (PRIV) __asm__ volatile("" ::"s"(pstash) : "memory");
+            __asm__ volatile("" ::: "memory");  // the values below come back from memory
         }
         intersect_scene<SCHED, COUNT>(S, o, d, go, id, err, ct, hyb_a, hyb_b, i == 0);
         if constexpr (STASH) {
+            if constexpr (PRIV) __asm__ volatile("" ::"s"(pstash) : "memory");
             __asm__ volatile("" ::: "memory");
-            auto gf = [&](int k) { return __uint_as_float(stash_get<ST>(L, k)); };
+#define gf(k) __uint_as_float(stash_get(k))
             ret = mk(gf(0), gf(1), gf(2));
             w = mk(gf(3), gf(4), gf(5));
             acc = mk(gf(6), gf(7), gf(8));
-            st = uint64_t(stash_get<ST>(L, 9)) | (uint64_t(stash_get<ST>(L, 10)) << 32);
-            casts = stash_get<ST>(L, 11); traced = stash_get<ST>(L, 12); hit_face = stash_get<ST>(L, 13);
+            st = uint64_t(stash_get(9)) | (uint64_t(stash_get(10)) << 32);
+            casts = stash_get(11); traced = stash_get(12); hit_face = stash_get(13);
             hit_t = gf(14);
         }
+#undef gf
+#undef stash_put
+#undef stash_get
         if (!go) continue;
         ++traced;
         if (record && i == 0) { hit_face = id.face; hit_t = id.t; }
@@ -1131,7 +1128,7 @@ __global__ __launch_bounds__(64 * sched_waves(SCHED), OCC) void render_kernel(Re
     // per-frame cameras (atr_render_start_cameras): fidx is wave-uniform, so the camera comes from
     // the kernel argument with scalar loads
     const atr_camera& cm = P.nfcam > 0 ? P.fcam[__builtin_amdgcn_readfirstlane(fidx)] : P.cam;
-    const DScene* S = P.scene;
+    const DScene* S = uniform_global(P.scene);  // global loads for materials, spheres, planes, shading
     int err = 0;
     Ctr ct;
     uint32_t casts = 0, traced = 0, hit_face = 0xFFFFFFFFu;

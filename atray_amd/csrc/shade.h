@@ -21,7 +21,7 @@ __device__ __forceinline__ void scene_finish(const DScene* __restrict__ S, V3 o,
     int32_t ns = -1, np = -1;
     const int32_t nspheres = __builtin_amdgcn_readfirstlane(S->nspheres), nplanes = __builtin_amdgcn_readfirstlane(S->nplanes);
     for (int32_t i = 0; i < nspheres; ++i) {  // sphere.h:12-39
-        const DSphere& sp = S->spheres[i];
+        const DSphere& sp = uniform_global(S->spheres)[i];
         const V3 pc = sub(o, mk(sp.cx, sp.cy, sp.cz));
         const float pcs = len2(pc);
         const float b = 2 * (dot(d, pc));
@@ -39,7 +39,7 @@ __device__ __forceinline__ void scene_finish(const DScene* __restrict__ S, V3 o,
         if (t > kTol && t < best) { best = t; ns = i; }
     }
     for (int32_t i = 0; i < nplanes; ++i) {  // plane.h:12-22
-        const DPlane& pl = S->planes[i];
+        const DPlane& pl = uniform_global(S->planes)[i];
         const V3 n = mk(pl.nx, pl.ny, pl.nz);
         const float denom = dot(n, d);
         float t = 0;
@@ -49,12 +49,12 @@ __device__ __forceinline__ void scene_finish(const DScene* __restrict__ S, V3 o,
     id.t = best;
     id.face = 0xFFFFFFFFu;
     if (np >= 0) {
-        const DPlane& pl = S->planes[np];
+        const DPlane& pl = as_global(S->planes)[np];
         id.type = T_PLANE;
         id.normal = mk(pl.nx, pl.ny, pl.nz);
         id.material = pl.material;
     } else if (ns >= 0) {
-        const DSphere& sp = S->spheres[ns];
+        const DSphere& sp = as_global(S->spheres)[ns];
         id.type = T_SPHERE;
         id.normal = sub(add(o, scale(d, best)), mk(sp.cx, sp.cy, sp.cz));  // Ray::at (ray.h:10-13)
         id.material = sp.material;
@@ -62,7 +62,7 @@ __device__ __forceinline__ void scene_finish(const DScene* __restrict__ S, V3 o,
         const DModel& m = S->models[nm];
         id.type = T_TRI;
         id.face = face;
-        const float* sh = m.shade + 9 * size_t(face);
+        const float* sh = as_global(m.shade) + 9 * size_t(face);
         if (m.smooth) {  // interpolated vertex normals (:129-138)
             const V3 na = mk(sh[0], sh[1], sh[2]), nb = mk(sh[3], sh[4], sh[5]), nc = mk(sh[6], sh[7], sh[8]);
             id.normal = add(add(scale(na, (1 - fu - fv)), scale(nb, fu)), scale(nc, fv));

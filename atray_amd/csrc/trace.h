@@ -37,6 +37,22 @@ __device__ __forceinline__ uint32_t first_active_lane() {
     return (threadIdx.x & 63) == uint32_t(__builtin_ctzll(__ballot(1))) ? 1u : 0u;
 }
 
+// Pointers into the scene's device tables are generic (loaded from memory): cast to the global
+// address space, the table loads are global loads instead of flat loads. uniform_global also
+// makes the value wave-uniform (readfirstlane: SGPRs) -- only for pointers every lane shares.
+template <class T>
+__device__ __forceinline__ T* as_global(T* p) {
+    using G = __attribute__((address_space(1))) T;
+    return (T*)(reinterpret_cast<G*>(reinterpret_cast<uint64_t>(p)));
+}
+template <class T>
+__device__ __forceinline__ T* uniform_global(T* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v)), hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    using G = __attribute__((address_space(1))) T;
+    return (T*)(reinterpret_cast<G*>((uint64_t(hi) << 32) | lo));
+}
+
 struct Ray {
     V3 o, d, inv;
     int s0, s1, s2;  // inv_signs (renderer.cpp:41-44)
