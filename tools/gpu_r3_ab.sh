@@ -15,3 +15,9 @@ python3 -c "import json; d=json.loads(open('$O/c3_$rep.json').read().strip().spl
 done
 timeout -k 10 300 python3 bench.py --config c4 --steps 8 --warmup 2 --no-pmc --no-cpu-baseline --no-prep --no-steady > $O/c4.json 2> $O/c4.err || { tail -20 $O/c4.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/c4.json').read().strip().splitlines()[-1]); print('c4', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'])"
+if [ -n "$AB_C4_VARIANTS" ]; then
+  for v in $AB_C4_VARIANTS; do
+    timeout -k 10 300 python3 bench.py --config c4 --steps 8 --warmup 2 --no-pmc --no-cpu-baseline --no-prep --no-steady --variant-code $v > $O/c4_$v.json 2> $O/c4_$v.err || { tail -20 $O/c4_$v.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/c4_$v.json').read().strip().splitlines()[-1]); print('c4 variant $v', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'])"
+  done
+fi
