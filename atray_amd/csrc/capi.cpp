@@ -38,7 +38,7 @@ extern "C" hipError_t atr_launch_packed_tile_casts(const int32_t* slot_tile, int
 
 extern "C" hipError_t atr_launch_plan(const atr::DBlock* base, int32_t nb, unsigned long long* cost,
                                       unsigned long long* cost_last, void* work, atr::DBlock* out, int32_t max_split,
-                                      hipStream_t s);
+                                      float split2, float split4, hipStream_t s);
 extern "C" size_t atr_plan_work_bytes(int32_t nb);
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s);
 extern "C" hipError_t atr_launch_scatter_bgr(const uint8_t* src, int64_t n, const int64_t* dst_index,
@@ -258,6 +258,7 @@ struct atr_ctx {
     // last launch per stream: everything this context has in flight (scene frees, workspace
     // regrowth and progressive group buffers wait for all of them)
     std::vector<std::pair<hipStream_t, hipEvent_t>> stream_ev;
+    int32_t wave_slots = 0;  // CUs x 4 SIMDs x 6 waves (single-frame plan policy), 0 until first use
 };
 
 namespace {
@@ -516,7 +517,19 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
         HIPCHK(hipEventRecord(c->ev_done, s));
         return ATR_OK;
     }
-    const int32_t max_split = std::max<int32_t>(1, nb / 25);  // spare blocks for splits (4 %)
+    // A launch whose cells fit the chip's wave slots at once (a shard's frame: 4,050 cells of an
+    // 8-way c3 plan vs 6,144 slots at 6 waves/SIMD) leaves slots idle while its heaviest cells
+    // finish: there the heaviest 3 % take four waves and the next 7 % two, which shortens the
+    // frame's critical path at no throughput cost. Larger launches split the heaviest 1 % in two.
+    if (!c->wave_slots) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        c->wave_slots = cus * 4 * 6;
+    }
+    const bool small = nb <= c->wave_slots;
+    const float split2 = small ? 0.10f : -1.f, split4 = small ? 0.03f : -1.f;
+    const int32_t max_split = std::max<int32_t>(1, small ? nb / 5 : nb / 25);  // spare blocks for splits
     int rc;
     const bool fresh = !bs->cost.p;  // the buffers start zeroed; each plan leaves them zeroed
     if ((rc = ensure_buf(bs->cost, size_t(nb) * sizeof(unsigned long long), true))) return rc;
@@ -536,7 +549,7 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
     HIPCHK(hipEventRecord(c->ev_done, s));
     HIPCHK(atr_launch_plan(static_cast<const DBlock*>(bs->dev.p), nb, static_cast<unsigned long long*>(bs->cost.p),
                            static_cast<unsigned long long*>(bs->cost_last.p), bs->plan_work.p,
-                           static_cast<DBlock*>(bs->plan_blocks.p), max_split, s));
+                           static_cast<DBlock*>(bs->plan_blocks.p), max_split, split2, split4, s));
     bs->plan_ready = true;
     bs->plan_stream = s;
     return ATR_OK;

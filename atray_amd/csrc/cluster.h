@@ -139,8 +139,10 @@ __device__ __forceinline__ bool cluster_pads(const Ray& r, const ScreenRay& sr, 
 
 // Screen of 8 primitives g .. g + 7 of n: words a0, a1 hold (nx, ny) of slots g .. g + 7 as f16,
 // z the nz of slots g .. g + 7 (two per word). Bit j: slot g + j needs the full test.
-// (The slots past n are masked off once per cluster by the caller, not per primitive.)
-__device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float dlo, float dhi, uint4_t a0, uint4_t a1,
+// Bit j set iff the f16 dot D_j of slot g + j lies in (blo, ahi]: the det band mapped back through
+// the cluster's step by the caller (cluster_cands). (The slots past n are masked off once per
+// cluster by the caller, not per primitive.)
+__device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float blo, float ahi, uint4_t a0, uint4_t a1,
                                             uint4_t z) {
     const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
@@ -152,8 +154,8 @@ __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nq, float
         // selects v_dot2c_f32_f16, whose accumulator is its destination, plus a v_mov of the zero
         float dz;
         asm("v_dot2_f32_f16 %0, %1, %2, 0" : "=v"(dz) : "v"((j & 1) ? sr.dz_hi : sr.dz_lo), "v"(pz));
-        const float e = __builtin_amdgcn_fdot2(sr.dxy, pxy, dz, false) * nq;
-        if (e >= dlo && e < dhi) gc |= 1u << j;
+        const float e = __builtin_amdgcn_fdot2(sr.dxy, pxy, dz, false);
+        if (e > blo && e <= ahi) gc |= 1u << j;
     }
     return gc;
 }
@@ -174,11 +176,22 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
     const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u;
     if constexpr (COUNT) ct.screen += n;
     const uint4_t* nb = m.cnrm + kClusterBlock * size_t(c);
-    const float nq = -hi.w;
+    const uint32_t slots = (2u << (n - 1)) - 1u;  // [0, n), 1 <= n <= 16
+    const float q = hi.w;
+    if (!(q >= 1.1754944e-38f)) return slots;  // zero or subnormal step (degenerate normals): no screen
+    // The band dlo <= -q D < dhi of the estimate, as a band of the dot D itself: D in
+    // (-dhi / q, -dlo / q] (one reciprocal per cluster instead of a product per primitive). The
+    // ends are widened by 2^-20 relative -- the hardware reciprocal (1 ulp) and the products'
+    // rounding are below 2^-22 -- and by 2^-126 absolute (flushed subnormals), so every primitive
+    // whose rounded product fell in the band still passes: the screen only grows.
+    const float rq = __builtin_amdgcn_rcpf(q);
+    const float a = -dlo * rq, b = -dhi * rq;  // b = -inf for the tight case (dhi = inf)
+    const float ahi = a + fabsf(a) * 9.5367432e-7f + 1.1754944e-38f;
+    const float blo = b - fabsf(b) * 9.5367432e-7f - 1.1754944e-38f;
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
-        cand |= screen8(sr, nq, dlo, dhi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8]) << g;
-    return cand & ((2u << (n - 1)) - 1u);  // slots [0, n), 1 <= n <= 16
+        cand |= screen8(sr, blo, ahi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8]) << g;
+    return cand & slots;
 }
 
 // Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and

@@ -30,8 +30,9 @@ constexpr int kPlanBuckets = 256;  // cost histogram: 8 buckets per power of two
 constexpr int kPlanClasses = 8;    // class index 0 (dispatched first) .. 7 (last)
 // cumulative fractions of the cells (heaviest first) that end classes 0, 1, ..., 6; the rest is 7
 __constant__ float kClassFrac[kPlanClasses - 1] = {0.02f, 0.05f, 0.10f, 0.20f, 0.30f, 0.50f, 0.75f};
-// the heaviest ATR_PLAN_SPLIT4 of the cells get four row-band waves, the heaviest ATR_PLAN_SPLIT2
-// two, within the list's spare capacity (max_split extra blocks)
+// default split fractions: the heaviest ATR_PLAN_SPLIT4 of the cells get four row-band waves, the
+// heaviest ATR_PLAN_SPLIT2 two, within the list's spare capacity (max_split extra blocks); the host
+// passes larger ones for launches that leave the chip's wave slots idle (capi.cpp launch_planned)
 constexpr float kSplit4Frac = ATR_PLAN_SPLIT4, kSplitFrac = ATR_PLAN_SPLIT2;
 
 struct Thresholds {
@@ -83,8 +84,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // it splits (whole buckets from the top while they fit the fraction and the spare capacity: both
 // conditions are monotone in b, so the split buckets are a top range, as a sequential walk would
 // take them); thr[k] = the lowest bucket of class k.
-__device__ void next_thresholds(const uint32_t* hist, int32_t nb, int32_t max_split, Thresholds& T,
-                                uint32_t* scratch /* 256 + 16 words of LDS */) {
+__device__ void next_thresholds(const uint32_t* hist, int32_t nb, int32_t max_split, float split2, float split4,
+                                Thresholds& T, uint32_t* scratch /* 256 + 16 words of LDS */) {
     const int b = int(threadIdx.x);
     const uint32_t n = hist[b];
     scratch[b] = n;  // inclusive suffix sum: cells in buckets >= b
@@ -101,14 +102,14 @@ __device__ void next_thresholds(const uint32_t* hist, int32_t nb, int32_t max_sp
     if (b < kPlanClasses + 2) thr[b] = kPlanBuckets;
     if (b == kPlanClasses + 2) thr[b] = 0;
     __syncthreads();
-    const bool s4 = n && float(incl) <= kSplit4Frac * float(nb) + 0.5f && 3u * incl <= uint32_t(max_split);
+    const bool s4 = n && float(incl) <= split4 * float(nb) + 0.5f && 3u * incl <= uint32_t(max_split);
     if (s4) {
         atomicMin(&thr[kPlanClasses + 1], b);
         atomicMax(&thr[kPlanClasses + 2], int32_t(incl));  // cells taking four waves
     }
     __syncthreads();
     const uint32_t n4 = uint32_t(thr[kPlanClasses + 2]);
-    const bool s2 = n && !s4 && float(incl) <= kSplitFrac * float(nb) + 0.5f &&
+    const bool s2 = n && !s4 && float(incl) <= split2 * float(nb) + 0.5f &&
                     3u * n4 + (incl - n4) <= uint32_t(max_split);
     if (s2 || s4) atomicMin(&thr[kPlanClasses], b);
     int k = 0;
@@ -132,7 +133,8 @@ __device__ void next_thresholds(const uint32_t* hist, int32_t nb, int32_t max_sp
 // Histogram + per-chunk class slots under W->use; the last workgroup derives W->next, the class
 // start slots and the used count, and clears the histogram for the next plan.
 __global__ __launch_bounds__(256) void plan_count_kernel(const unsigned long long* __restrict__ cost, int32_t nb,
-                                                         int32_t max_split, PlanWork* __restrict__ W,
+                                                         int32_t max_split, float split2, float split4,
+                                                         PlanWork* __restrict__ W,
                                                          uint32_t* __restrict__ chunk_slots) {
     __shared__ uint32_t h[kPlanBuckets];
     __shared__ uint32_t scratch[kPlanBuckets + 16];
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(256) void plan_count_kernel(const unsigned long lon
         W->done_count = 0;
     }
     __shared__ Thresholds nx;
-    next_thresholds(h, nb, max_split, nx, scratch);
+    next_thresholds(h, nb, max_split, split2, split4, nx, scratch);
     if (threadIdx.x == 0) W->next = nx;
 }
 
@@ -284,14 +286,18 @@ __global__ __launch_bounds__(256) void plan_order_kernel(const DBlock* __restric
 // plan by every plan (a zeroed `use` = one class, no split, until the first plan promotes real
 // thresholds); cost: the render's per-base-block clocks (cleared again; cost_last keeps them); out:
 // cap = nb + max_split blocks.
+// split2 / split4 < 0: the defaults (ATR_PLAN_SPLIT2 / ATR_PLAN_SPLIT4).
 extern "C" hipError_t atr_launch_plan(const atr::DBlock* base, int32_t nb, unsigned long long* cost,
                                       unsigned long long* cost_last, void* work, atr::DBlock* out, int32_t max_split,
-                                      hipStream_t s) {
+                                      float split2, float split4, hipStream_t s) {
+    if (split2 < 0.f) split2 = atr::kSplitFrac;
+    if (split4 < 0.f) split4 = atr::kSplit4Frac;
     if (nb <= 0) return hipSuccess;
     atr::PlanWork* W = static_cast<atr::PlanWork*>(work);
     uint32_t* chunk_slots = reinterpret_cast<uint32_t*>(W + 1);
     const unsigned g = unsigned((nb + 255) / 256);
-    hipLaunchKernelGGL(atr::plan_count_kernel, dim3(g), dim3(256), 0, s, cost, nb, max_split, W, chunk_slots);
+    hipLaunchKernelGGL(atr::plan_count_kernel, dim3(g), dim3(256), 0, s, cost, nb, max_split, split2, split4, W,
+                       chunk_slots);
     hipLaunchKernelGGL(atr::plan_order_kernel, dim3(g), dim3(256), 0, s, base, nb, cost, cost_last, W, chunk_slots,
                        out, nb + max_split);
     return hipGetLastError();

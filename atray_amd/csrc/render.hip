@@ -765,13 +765,14 @@ __device__ __forceinline__ void tree_closest_tile(const Ray& r, const DModel& m,
 // ------------------------------------------------------------------ get_intersection_data
 enum { SCHED_LANE = 0, SCHED_WAVE = 1, SCHED_TILE4 = 2, SCHED_TILE8 = 3, SCHED_CLUSTER = 4, SCHED_CLUSTER_K4 = 5,
        SCHED_FLAT = 6, SCHED_HYBRID = 7, SCHED_FLAT_NOCC = 9, SCHED_HYBRID_NOCC = 10, SCHED_FLAT_UT = 11,
-       SCHED_FLAT_REGEN = 12 };
+       SCHED_FLAT_REGEN = 12, SCHED_FLAT_ONE = 13 };
 // The FLAT / HYBRID family (wave-wide leaf steps, LDS path stash). FLAT and HYBRID compact the full
 // tests' candidates over the wavefront (cand_rounds); the _NOCC schedules are the round-2 kernels
 // that test a cluster's candidates in its lane (diagnostic); FLAT_UT walks every
 // bounce's DFS passes wave-wide (diagnostic).
 constexpr bool sched_flat(int sc) {
-    return sc == SCHED_FLAT || sc == SCHED_FLAT_NOCC || sc == SCHED_FLAT_UT || sc == SCHED_FLAT_REGEN;
+    return sc == SCHED_FLAT || sc == SCHED_FLAT_NOCC || sc == SCHED_FLAT_UT || sc == SCHED_FLAT_REGEN ||
+           sc == SCHED_FLAT_ONE;
 }
 constexpr bool sched_hyb(int sc) { return sc == SCHED_HYBRID || sc == SCHED_HYBRID_NOCC; }
 constexpr bool sched_cc(int sc) { return sc != SCHED_FLAT_NOCC && sc != SCHED_HYBRID_NOCC; }
@@ -823,9 +824,9 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (sched_flat(SCHED)) {
                 constexpr bool CC = sched_cc(SCHED);
                 // the camera rays of a bounce loop (one origin, coherent) take HYBRID's primary flavour
-                if (first)
+                if (first && SCHED != SCHED_FLAT_ONE)  // FLAT_ONE (diagnostic): one flavour for every bounce
                     tree_closest_flat<COUNT, true, true, false, true, true, false, CC>(r, m, active, h, err, ct, hyb_a, hyb_b);
-                else if constexpr (SCHED == SCHED_FLAT || SCHED == SCHED_FLAT_REGEN)  // LDS leaf buffer: fewer VGPRs, 5 waves/SIMD (§4d)
+                else if constexpr (SCHED == SCHED_FLAT || SCHED == SCHED_FLAT_REGEN || SCHED == SCHED_FLAT_ONE)  // LDS leaf buffer: fewer VGPRs, 5 waves/SIMD (§4d)
                     tree_closest_flat<COUNT, false, true, true, false, false, false, true>(r, m, active, h, err, ct);
                 else if constexpr (SCHED == SCHED_FLAT_UT)
                     tree_closest_flat<COUNT, false, true, true, false, true, false, CC>(r, m, active, h, err, ct);
@@ -881,7 +882,7 @@ __device__ __forceinline__ V3 cast_ray(const DScene* __restrict__ S, V3 o, V3 d,
                                        uint32_t& traced, bool record, uint32_t& hit_face, float& hit_t,
                                        int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b, V3& acc) {
     constexpr bool STASH = sched_flat(SCHED) || sched_hyb(SCHED);
-    constexpr bool PRIV = SCHED == SCHED_FLAT;  // the stash in private memory (above)
+    constexpr bool PRIV = SCHED == SCHED_FLAT || SCHED == SCHED_FLAT_ONE;  // the stash in private memory (above)
     __shared__ uint32_t s_stash[STASH && !PRIV ? 4 : 1][PRIV ? 1 : kStash][64];
     // the private stash is indexed directly (scratch loads and stores); through a generic pointer
     // every access was a flat load or store
@@ -1287,6 +1288,9 @@ ATR_INST(SCHED_FLAT_NOCC, false, false) ATR_INST(SCHED_FLAT_NOCC, true, false)
 ATR_INST(SCHED_FLAT_UT, false, false) ATR_INST(SCHED_FLAT_UT, true, false)
 ATR_INST4(SCHED_FLAT_REGEN)
 template __global__ void render_kernel<SCHED_FLAT_REGEN, false, false, 5>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT_ONE, false, false, 6>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT_ONE, false, false, 7>(RenderParams);
+template __global__ void render_kernel<SCHED_FLAT_ONE, true, false>(RenderParams);
 ATR_INST(SCHED_HYBRID_NOCC, true, true) ATR_INST(SCHED_HYBRID_NOCC, true, false)
 ATR_INST(SCHED_HYBRID_NOCC, false, false)
 
@@ -1422,6 +1426,11 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, h
             if (sched == 102 && !prim && !count)
                 hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT_REGEN, false, false, 5>), g, b, 0, s, P);
             else launch_sched<atr::SCHED_FLAT_REGEN>(P, count, prim, s);
+        } else if (sched == 106 || sched == 107) {  // FLAT_ONE at 6 / 7 waves/SIMD (bounce loops only)
+            if (prim) return hipErrorInvalidValue;
+            if (count) launch_one<atr::SCHED_FLAT_ONE, true, false>(P, s);
+            else if (sched == 106) hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT_ONE, false, false, 6>), g, b, 0, s, P);
+            else hipLaunchKernelGGL((atr::render_kernel<atr::SCHED_FLAT_ONE, false, false, 7>), g, b, 0, s, P);
         } else if (sched == 100) {
             if (prim) return hipErrorInvalidValue;
             if (count) launch_one<atr::SCHED_FLAT_UT, true, false>(P, s);

@@ -21,3 +21,9 @@ if [ -n "$AB_C4_VARIANTS" ]; then
     python3 -c "import json; d=json.loads(open('$O/c4_$v.json').read().strip().splitlines()[-1]); print('c4 variant $v', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'])"
   done
 fi
+if [ -n "$AB_SIM_RANKS" ]; then
+  for r in $AB_SIM_RANKS; do
+    timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline --no-prep --no-steady --sim-world 8 --sim-rank $r > $O/c3sim_$r.json 2> $O/c3sim_$r.err || { tail -20 $O/c3sim_$r.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/c3sim_$r.json').read().strip().splitlines()[-1]); print('c3 shard $r', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'])"
+  done
+fi
