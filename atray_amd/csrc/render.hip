@@ -313,7 +313,7 @@ __device__ __forceinline__ FlatLds& flat_lds() {
 // and barycentrics.
 template <bool COUNT, bool UO, bool NUV>
 __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
-                                            uint32_t cfirst, int32_t own, Ctr& ct);
+                                            uint32_t cfirst, int32_t own, Ctr& ct, int32_t vr = 0, bool spec = false);
 
 // HYB (the HYBRID schedule): each step the wavefront decides, uniformly, how to scan its rays'
 // current leaves: lane-private (every lane scans its own leaf's clusters, as CLUSTER does: no
@@ -323,9 +323,11 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
 // hyb_a / hyb_b). A leaf's result does not depend on how its clusters were visited (minimum
 // (t, leaf rank)), so the choice changes no output bit. LDSB: the DFS pass inserts straight
 // into the LDS columns (CLUSTER's LdsLeafBuf) instead of a register buffer copied after it.
+// own: the candidates' owner slot (its key in LDS); with speculative leaf steps (spec) a slot is a
+// (ray, leaf) pair and vr the ray lane of this lane's slot, so the ray comes from lane vr[own].
 template <bool COUNT, bool UO, bool NUV>
 __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
-                                            uint32_t cfirst, int32_t own, Ctr& ct) {
+                                            uint32_t cfirst, int32_t own, Ctr& ct, int32_t vr, bool spec) {
     constexpr unsigned long long kInit = (static_cast<unsigned long long>(0x7F7FFFFFu) << 32) | 0xFFFFFFFFull;
     FlatLds& L = flat_lds();
     const uint32_t cc = uint32_t(__popc(cm));
@@ -353,9 +355,10 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
         b += j >= (x & 1u) ? 1u : 0u;
         const uint32_t slot = uint32_t(__shfl(int(cfirst), s2)) + b;
         const int32_t ow = __shfl(own, s2);
+        const int32_t rw = spec ? __shfl(vr, ow) : ow;  // the lane holding the owner's ray
         Ray q;
-        q.o = UO ? r.o : mk(shfl_f(r.o.x, ow), shfl_f(r.o.y, ow), shfl_f(r.o.z, ow));
-        q.d = mk(shfl_f(r.d.x, ow), shfl_f(r.d.y, ow), shfl_f(r.d.z, ow));
+        q.o = UO ? r.o : mk(shfl_f(r.o.x, rw), shfl_f(r.o.y, rw), shfl_f(r.o.z, rw));
+        q.d = mk(shfl_f(r.d.x, rw), shfl_f(r.d.y, rw), shfl_f(r.d.z, rw));
         unsigned long long mine = kInit;
         bool imp = false;
         float u = 0.f, v = 0.f;
@@ -385,8 +388,22 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
     }
 }
 
+// Speculative leaf steps (SPEC; experiment build -DATR_SPEC, not kept: DESIGN.md §4g measured it
+// 4% slower on c3 and c4 with no latency gain): when at most 64 / kSpecLeaves rays of the wave are
+// still scanning (the tail of a slow cell: a few grazing rays walking many leaves one dependent
+// step at a time), each takes its next kSpecLeaves leaves in one step, one (ray, leaf) slot per
+// lane. Every leaf is scanned from a fresh best, exactly as alone, and the ray takes the first of
+// them (buffer order) that improved its hit (kd_tree.cpp:457-460), so the result is the
+// sequential one; the leaves after it were speculative work on lanes that would have idled.
+constexpr int kSpecLeaves = 4;
+#ifdef ATR_SPEC
+constexpr bool kSpecOn = true;
+#else
+constexpr bool kSpecOn = false;
+#endif
+
 template <bool COUNT, bool HYB = false, bool LDSB = false, bool PAIR = true, bool UO = false, bool UT = false,
-          bool NUV = false, bool CC = false>
+          bool NUV = false, bool CC = false, bool SPEC = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
@@ -464,11 +481,31 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         }
         ATR_PCLK(const uint64_t tc2 = clock64());
         ATR_PCLK(ct.t_pass += uint32_t(tc2 - tc0));
-        if (__ballot(!done) == 0) break;
+        const uint64_t livem = __ballot(!done);
+        if (livem == 0) break;
         // every live ray's current leaf: its clusters are this step's items
         int32_t leaf = -1;
         uint32_t cf = 0, cn = 0;
-        if (!done) {
+        bool spec = false;  // wave-uniform
+        int32_t vr = ln;    // the ray lane of this lane's (ray, leaf) slot
+        if constexpr (SPEC) spec = __popcll(livem) <= uint32_t(64 / kSpecLeaves);
+        if (spec) {
+            // slot q * kSpecLeaves + k: the q-th live ray's k-th next leaf
+            if (!done) s_mark[w][__popcll(livem & ((uint64_t(1) << ln) - 1))] = ln;
+            __builtin_amdgcn_wave_barrier();
+            const int32_t qv = ln / kSpecLeaves, kv = ln % kSpecLeaves;
+            vr = qv < int32_t(__popcll(livem)) ? s_mark[w][qv] : -1;
+            __builtin_amdgcn_wave_barrier();
+            const int32_t rs = vr >= 0 ? vr : ln;
+            const int32_t jr = __shfl(j, rs) + kv, nbr = __shfl(nb, rs);
+            if (vr >= 0 && jr < nbr) {
+                leaf = s_lbl[w][jr][vr];
+                const uint2_t cr = load_range(m.cl_range, leaf);
+                cf = cr.x;
+                cn = cr.y;
+            }
+            if (vr < 0) vr = ln;
+        } else if (!done) {
             leaf = s_lbl[w][j][ln];
             const uint2_t cr = load_range(m.cl_range, leaf);
             cf = cr.x;
@@ -480,7 +517,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
         s_key[w][ln] = kInit;
         bool deal = true;
-        if constexpr (HYB) {
+        if constexpr (HYB) if (!spec) {
             // the largest cluster count of the step (counts are small: the signed max is exact)
             const uint32_t mx = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
             deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
@@ -533,11 +570,12 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             const bool valid = k < total;
             if constexpr (COUNT) { ct.round_wave += ln == 0 ? 1u : 0u; ct.round_items += valid ? 1u : 0u; }
             const int32_t src = valid ? own : ln;
+            const int32_t rsrc = spec ? __shfl(vr, src) : src;  // the lane holding the owner's ray
             Ray q;  // the owner's ray
             // UO: every ray of the wave starts at the same point (primary rays: the frame's eye)
-            q.o = UO ? r.o : mk(shfl_f(r.o.x, src), shfl_f(r.o.y, src), shfl_f(r.o.z, src));
-            q.d = mk(shfl_f(r.d.x, src), shfl_f(r.d.y, src), shfl_f(r.d.z, src));
-            q.inv = mk(shfl_f(r.inv.x, src), shfl_f(r.inv.y, src), shfl_f(r.inv.z, src));
+            q.o = UO ? r.o : mk(shfl_f(r.o.x, rsrc), shfl_f(r.o.y, rsrc), shfl_f(r.o.z, rsrc));
+            q.d = mk(shfl_f(r.d.x, rsrc), shfl_f(r.d.y, rsrc), shfl_f(r.d.z, rsrc));
+            q.inv = mk(shfl_f(r.inv.x, rsrc), shfl_f(r.inv.y, rsrc), shfl_f(r.inv.z, rsrc));
             q.s0 = q.inv.x < 0;
             q.s1 = q.inv.y < 0;
             q.s2 = q.inv.z < 0;
@@ -549,7 +587,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                     cm = cluster_cands<COUNT>(q, m, c, m.clus[kClusterBlock * size_t(c)],
                                               m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
                 }
-                cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
+                cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct, vr, spec);
                 continue;
             }
             unsigned long long mine = kInit;
@@ -581,7 +619,37 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             __builtin_amdgcn_wave_barrier();
         }
         ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
-        if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
+        if (spec) {
+            if (!done) {  // the first of this ray's slots (buffer order) whose leaf improved the hit
+                const int32_t q0 = int32_t(__popcll(livem & ((uint64_t(1) << ln) - 1))) * kSpecLeaves;
+                bool imp = false;
+                for (int32_t kk = 0; kk < kSpecLeaves && j + kk < nb; ++kk) {
+                    const unsigned long long key = s_key[w][q0 + kk];
+                    if (key != kInit) {
+                        imp = true;
+                        res_t = __uint_as_float(uint32_t(key >> 32));
+                        res_slot = s_slot[w][q0 + kk];
+                        if constexpr (!NUV) {
+                            res_u = s_u[w][q0 + kk];
+                            res_v = s_v[w][q0 + kk];
+                        }
+                        break;
+                    }
+                }
+                if (imp) {
+                    done = true;
+                } else {  // none did: the re-walk bound is the last leaf scanned
+                    const int32_t last = (j + kSpecLeaves < nb ? j + kSpecLeaves : nb) - 1;
+                    bd = s_lbd[w][last][ln];
+                    bi = s_lbl[w][last][ln];
+                    j = last + 1;
+                    if (j >= nb) {
+                        if (more) need = true;
+                        else done = true;
+                    }
+                }
+            }
+        } else if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
             bool imp = lp_imp;
             if (deal || CC) {
                 const unsigned long long key = s_key[w][ln];
@@ -825,9 +893,11 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                 constexpr bool CC = sched_cc(SCHED);
                 // the camera rays of a bounce loop (one origin, coherent) take HYBRID's primary flavour
                 if (first && SCHED != SCHED_FLAT_ONE)  // FLAT_ONE (diagnostic): one flavour for every bounce
-                    tree_closest_flat<COUNT, true, true, false, true, true, false, CC>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                    tree_closest_flat<COUNT, true, true, false, true, true, false, CC, CC && !COUNT && kSpecOn>(
+                        r, m, active, h, err, ct, hyb_a, hyb_b);
                 else if constexpr (SCHED == SCHED_FLAT || SCHED == SCHED_FLAT_REGEN || SCHED == SCHED_FLAT_ONE)  // LDS leaf buffer: fewer VGPRs, 5 waves/SIMD (§4d)
-                    tree_closest_flat<COUNT, false, true, true, false, false, false, true>(r, m, active, h, err, ct);
+                    tree_closest_flat<COUNT, false, true, true, false, false, false, true, !COUNT && kSpecOn>(
+                        r, m, active, h, err, ct);
                 else if constexpr (SCHED == SCHED_FLAT_UT)
                     tree_closest_flat<COUNT, false, true, true, false, true, false, CC>(r, m, active, h, err, ct);
                 else tree_closest_flat<COUNT, false, false, true, false, false, false, CC>(r, m, active, h, err, ct);
@@ -835,7 +905,8 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
             else if constexpr (sched_hyb(SCHED))
                 // primary rays: LDS leaf buffer, one candidate test at a time (fewer VGPRs, as CLUSTER);
                 // bounces: FLAT's register buffer and paired candidate loads (measured)
-                tree_closest_flat<COUNT, true, PR, !PR, PR, PR, PR, sched_cc(SCHED)>(r, m, active, h, err, ct, hyb_a, hyb_b);
+                tree_closest_flat<COUNT, true, PR, !PR, PR, PR, PR, sched_cc(SCHED),
+                                  sched_cc(SCHED) && !COUNT && kSpecOn>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (SCHED == SCHED_TILE4) tree_closest_tile<4, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_TILE8) tree_closest_tile<8, COUNT>(r, m, active, h, err, ct);
             else if constexpr (SCHED == SCHED_CLUSTER) {

@@ -9,7 +9,7 @@ HB=$!
 trap "kill $HB" EXIT
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_C3_REPS:-2}); do
 timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-prep --no-steady > $O/c3_$rep.json 2> $O/c3_$rep.err || { tail -20 $O/c3_$rep.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/c3_$rep.json').read().strip().splitlines()[-1]); r=d['roofline']; print('c3', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'], r.get('valu',{}).get('wave_insts_per_frame'), r.get('frac'))"
 done
