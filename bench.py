@@ -270,6 +270,8 @@ def main():
     ap.add_argument("--cell-order", default="graded", choices=["list", "graded"],
                     help="graded (default): cells dispatched by the calibration frames' measured cost, heaviest "
                          "class first (atr_set_cell_plan classes); list: tile list order (Morton within a tile)")
+    ap.add_argument("--cell-prio", type=float, default=0.0,
+                    help="with --cell-order graded: the heaviest FRAC of the cells issue at raised wave priority")
     ap.add_argument("--stream-priority", type=int, default=-1,
                     help="1: stream 0 at the device's highest priority (its launch completes first, so at N > 1 "
                          "its exchange overlaps the other launches' rendering); -1 (default) = on for N > 1")
@@ -496,7 +498,10 @@ def run(args):
                 cls[crank >= int(round(f * live))] = 6 - k
             cls[crank < int(round(bounds[0] * live))] = 7
             cplan |= (cls << 4).astype(np.uint8)
+            if args.cell_prio > 0:  # the heaviest cells' waves also issue first on their SIMD
+                cplan[crank < int(round(args.cell_prio * live))] |= 0x80  # ATR_PLAN_PRIO
             cell_split["order"] = args.cell_order
+            cell_split["prio_frac"] = args.cell_prio
         eng.set_cell_plan(W, H, cplan)
     if pw > 1 or args.single_tiles == "cost":
         tiles = E.tiles_array(plan.tiles[pr])
