@@ -23,8 +23,9 @@ with open(f"{P}/trace_c3_driver_summary.json", "w") as f:
     subprocess.run([sys.executable, f"{R}/tools/trace_summary.py", f"{G}/r3c/trace_driver"], stdout=f, check=True)
 lines = open(f"{G}/r3c/pytest_gpu.log").read().strip().splitlines()
 open(f"{P}/pytest_gpu_tail.txt", "w").write("\n".join(lines[-2:]) + "\n")
-if os.path.exists(f"{G}/r3c/bench_c4.json"):
-    shutil.copy(f"{G}/r3c/bench_c4.json", f"{P}/bench_c4_nopmc.json")
+for src, dst in (("bench_c4_full.json", "bench_c4.json"), ("bench_c5_full.json", "bench_c5.json")):
+    if os.path.exists(f"{G}/r3c/{src}"):
+        shutil.copy(f"{G}/r3c/{src}", f"{P}/{dst}")
 pmc = {}
 for p in sorted(glob.glob(f"{G}/bench_pmc/pass*")):
     for r in csv.DictReader(open(p + "/pmc_counter_collection.csv")):
