@@ -435,11 +435,12 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
         if (hipMalloc(&b.dev_tiles.p, tneed) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
         b.dev_tiles.n = tneed;
     }
-    {   // pixel of every packed slot, in slot order
+    {   // pixel of every packed slot: a block's pixels occupy out_base.. in lane order (a cell
+        // plan's classes reorder the list, not the slots)
         std::vector<int32_t> pix(size_t(b.packed_pixels > 0 ? b.packed_pixels : 1), 0);
-        size_t k = 0;
         for (const DBlock& blk : b.host) {
             const uint64_t m = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+            size_t k = size_t(blk.out_base);
             for (int lane = 0; lane < 64; ++lane)
                 if ((m >> lane) & 1) pix[k++] = (blk.y0 + (lane >> 3)) * W + (blk.x0 + (lane & 7));
         }
@@ -1732,9 +1733,9 @@ int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles,
                 }
         }
         std::vector<int32_t> st(size_t(n > 0 ? n : 1), -1);
-        size_t k = 0;
-        for (const DBlock& blk : bs->host) {
+        for (const DBlock& blk : bs->host) {  // slots out_base.. in lane order (not list order)
             const uint64_t m = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+            size_t k = size_t(blk.out_base);
             for (int lane = 0; lane < 64; ++lane)
                 if ((m >> lane) & 1)
                     st[k++] = owner[size_t(blk.y0 + (lane >> 3)) * size_t(width) + size_t(blk.x0 + (lane & 7))];

@@ -161,18 +161,35 @@ def test_reference_tiles_and_ray_cast_counts(eng):
 
 
 @pytest.mark.parametrize("kind", ["shard", "reference"])
-def test_packed_tile_ray_casts(eng, kind):
+@pytest.mark.parametrize("planned", [False, True])
+def test_packed_tile_ray_casts(eng, kind, planned):
     """atr_packed_tile_ray_casts (the multi-GPU bench's per-tile counters): per-tile sums of a
     PACKED multi-frame ray_casts buffer equal the sums of the golden per-pixel ray_casts over each
     tile's pixels -- shard tiles (disjoint), and the reference's overlapping tiles, where a pixel
-    counts in the first tile holding it (the packed layout traces it once)."""
+    counts in the first tile holding it (the packed layout traces it once). planned: a cell plan
+    with dispatch classes and splits reorders the block list, not the packed slots (the bench's
+    graded order; the slot-to-tile map once followed the list order)."""
     name = "monkey_320x180_s4_b5"
     g = GOLD["render"][name]
     upload(eng, "Monkey", True)
     W, H = g["W"], g["H"]
     cam = E.camera(W, H, g["spp"], g["bounces"])
     tiles = E.make_shard_tiles(W, H, 32, 1, 3) if kind == "shard" else E.make_tiles(W, H, 8)
-    o = run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED)
+    if planned:
+        rng = np.random.default_rng(11)
+        ncell = ((W + 7) // 8) * ((H + 7) // 8)
+        plan = rng.choice(np.array([0, 2, E.plan_class(7), E.plan_class(4) | 4, E.plan_class(1)], np.uint8),
+                          size=ncell)
+        eng.set_cell_plan(W, H, plan)
+    try:
+        o = run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED)
+        _check_packed_tile_casts(eng, name, W, H, tiles, o)
+    finally:
+        if planned:
+            eng.set_cell_plan(W, H, None)
+
+
+def _check_packed_tile_casts(eng, name, W, H, tiles, o):
     n = E.packed_size(tiles)
     F, stride = 3, n + 11
     casts = torch.full((F * stride,), 5, dtype=torch.int32, device="cuda")
