@@ -195,7 +195,7 @@ atr_tuning default_tuning() {
     t.xcd_chunk = 16;      // chunks of 16 cells per XCD, interleaved
     t.frame_rotate = 0;    // §4b: rotation measured slower
     t.hybrid_a = 2;        // §4e: sweep optimum
-    t.hybrid_b = 1;
+    t.hybrid_b = 0;
     t.persist_chunk = 16;  // §4c
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
     t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs

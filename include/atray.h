@@ -163,7 +163,7 @@ typedef struct {
     int32_t frame_rotate;   /* multi-frame launches: frame f's cell list starts f/F x this/1024 of
                                the way in, 0..1024; default 0 */
     int32_t hybrid_a, hybrid_b; /* HYBRID: a leaf step is dealt over the lanes when the largest
-                               cluster count exceeds a x rounds + b, -4096..4096; default 2, 1 */
+                               cluster count exceeds a x rounds + b, -4096..4096; default 2, 0 */
     int32_t persist_chunk;  /* PERSIST: 8x8 cells per work-queue claim, 1..4096; default 16 */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
     int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
