@@ -540,3 +540,34 @@ def test_bgr_exchange_reassembles_frames(eng):
     for f in range(F):
         full = run(eng, cams[f])
         assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
+
+
+def test_block_cache_eviction_waits_for_every_stream(eng):
+    """A tile list's cached block set read by launches on two streams is rewritten only after both
+    have finished (round-2 advice: the slot's event once covered only the later stream): a long
+    PACKED multi-bounce render on stream A, a short render of the same tiles on stream B, then
+    more distinct tile lists on B than the cache holds (24), which evicts the set while A may
+    still run. A's frame must equal the same render on an idle GPU."""
+    upload(eng, "Dragon", True)
+    W, H = 480, 270
+    cam = E.camera(W, H, 16, 5)
+    tiles = E.make_shard_tiles(W, H, 64, 0, 2)
+    want = run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED)
+    n = E.packed_size(tiles)
+    dev = torch.device("cuda", 0)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    fa = torch.full((n,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
+    ca = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    eng.render_start(cam, tiles, E.atr_frame(E.ATR_LAYOUT_PACKED, fa.data_ptr(), None, None, None, ca.data_ptr(),
+                                             None), SEED, stream=sa.cuda_stream)
+    fb = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    frb = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, None, None)
+    small = E.camera(W, H)
+    eng.render_start(small, tiles, frb, SEED, stream=sb.cuda_stream)
+    for k in range(30):
+        eng.render_start(small, [[k, 0, W - 1 - k, H - 1]], frb, SEED, stream=sb.cuda_stream)
+    torch.cuda.synchronize()
+    rc, _ = eng.wait()
+    assert rc == 0
+    assert np.array_equal(fa.cpu().numpy().view(np.uint32), want["fb"])
+    assert np.array_equal(ca.cpu().numpy().view(np.uint32), want["casts"])
