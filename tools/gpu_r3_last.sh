@@ -1,0 +1,12 @@
+#!/bin/bash
+# Last check at HEAD: the whole GPU suite, smoke, and the driver's bench command.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r3last
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], d['single_frame']['latency_ms'], r['frac'], r['valu']['frac'], r['valu']['wave_insts_per_frame'], d['speedup_vs_cpu'])"
