@@ -19,17 +19,19 @@
 
 #include "engine.h"
 #include "host_scene.h"
-#include "wavefront.h"
+#ifdef ATR_DIAG
+#include "../../include/atray_diag.h"
+#endif
 
 using namespace atr;
 
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s);
-extern "C" hipError_t atr_launch_persist(const atr::RenderParams& P, int ncu, hipStream_t s);
 extern "C" hipError_t atr_launch_traced_finish(unsigned long long* slots, unsigned long long* out, hipStream_t s);
 extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                         const uint32_t* packed, uint32_t* image, hipStream_t s);
-extern "C" hipError_t atr_wf_render(const atr::WFParams& W, int32_t nmodels, const int32_t* nnodes,
-                                    const int32_t* has_tree, int32_t* pinned, hipStream_t s);
+extern "C" hipError_t atr_launch_path_camera(const atr::PathParams& P, int occ, hipStream_t s);
+extern "C" hipError_t atr_launch_path_bounce(const atr::PathParams& P, int ncu, int occ, hipStream_t s);
+extern "C" hipError_t atr_launch_path_resolve(const atr::PathParams& P, hipStream_t s);
 extern "C" hipError_t atr_launch_tile_casts(const atr_tile* tiles, int32_t ntiles, int32_t width,
                                             const uint32_t* casts, int64_t* out, hipStream_t s);
 extern "C" hipError_t atr_launch_packed_tile_casts(const int32_t* slot_tile, int64_t nslots, const uint32_t* casts,
@@ -65,7 +67,6 @@ struct BlockSet {
     std::vector<DBlock> host;
     DevBuf dev;
     DevBuf dev_tiles;
-    DevBuf dev_pix;  // pixel index per packed slot (wavefront schedule)
     uint32_t cplan_gen = 0;  // the ctx's cell plan this set was built with
     DevBuf dev_tile;  // owning tile per packed slot (atr_packed_tile_ray_casts; built on first use)
     bool tile_ready = false;
@@ -196,14 +197,14 @@ atr_tuning default_tuning() {
     t.frame_rotate = 0;    // §4b: rotation measured slower
     t.hybrid_a = 2;        // §4e: sweep optimum
     t.hybrid_b = 0;
-    t.persist_chunk = 16;  // §4c
+    t.path_batch_log2 = 27;  // §4h: 2^27 paths per batch (c4: one batch per frame)
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
     t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs
     return t;
 }
-constexpr int kSchedPersist = 8;
-constexpr int kQueueSlots = 32;             // queue-head sets in flight (ring)
-constexpr size_t kQueueBytes = 8 * 32 * 4;  // 8 heads, 128 B apart
+constexpr int kSchedPaths = 10;             // the sample-parallel path engine (paths.hip)
+constexpr int kMaxPathBounces = 64;         // bounce launches per batch (AUTO: deeper paths run FLAT)
+constexpr int kQueueSlots = 32;             // traced-ray counter sets in flight (ring)
 constexpr size_t kTraceBytes = 64 * 128;    // 64 traced-ray counters, 128 B apart (render.hip)
 
 }  // namespace
@@ -231,20 +232,18 @@ struct atr_ctx {
     uint64_t block_use[kBlockSlots] = {};
     uint64_t use_clock = 0;
     int32_t* d_error = nullptr;
-    // wavefront workspace (grown on demand)
-    DevBuf wf_mem;
-    int64_t wf_n = 0, wf_nodes = 0;
-    atr::WFParams wf = {};
-    int32_t* wf_pinned = nullptr;
-    std::vector<int32_t> model_nodes, model_tree;
-    // PERSIST work-queue heads: a ring of sets, each zeroed on the launch stream before use and
-    // reused only after the launch that last used it (event) has finished
     int ncu = 256;
-    void* qring = nullptr;
-    hipEvent_t qev[kQueueSlots] = {};
-    bool qused[kQueueSlots] = {};
-    int qnext = 0;
-    // cell launches' traced-ray counter sets (same ring discipline, zeroed by their finish kernel)
+    // path engine workspace per stream (paths.hip: two path queues, the per-path results and the
+    // per-level counters), grown on demand
+    struct PathWS {
+        hipStream_t stream = nullptr;
+        DevBuf mem;
+        int64_t cap = 0;
+        int32_t levels = 0;
+    };
+    std::vector<PathWS> path_ws;
+    // launches' traced-ray counter sets: a ring, each set reused only after the launch that last
+    // used it (event) has finished; zeroed by its finish kernel
     void* tring = nullptr;
     hipEvent_t tev[kQueueSlots] = {};
     bool tused[kQueueSlots] = {};
@@ -324,69 +323,6 @@ hipError_t note_launch(atr_ctx* c, hipStream_t s, BlockSet* bs) {
 // Wait for every launch of this context still in flight, on any stream.
 hipError_t wait_all(atr_ctx* c) { return wait_list(c->stream_ev); }
 
-// Carve the wavefront workspace for n path slots and a tree of `nodes` nodes.
-int wf_reserve(atr_ctx* c, int64_t n, int64_t nodes) {
-    if (n <= c->wf_n && nodes <= c->wf_nodes && c->wf_mem.p) return ATR_OK;
-    HIPCHK(wait_all(c));
-    if (c->wf_mem.p) HIPCHK(hipFree(c->wf_mem.p));
-    c->wf_mem = DevBuf();
-    n = std::max<int64_t>(n, c->wf_n);
-    nodes = std::max<int64_t>(nodes, c->wf_nodes);
-    size_t off = 0;
-    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-    const size_t o_rng = take(8 * n), o_col = take(12 * n), o_ret = take(12 * n), o_wt = take(12 * n),
-                 o_casts = take(4 * n), o_traced = take(4 * n), o_hface = take(4 * n), o_ht = take(4 * n),
-                 o_ro = take(12 * n), o_rd = take(12 * n), o_bt = take(4 * n), o_bu = take(4 * n),
-                 o_bv = take(4 * n), o_bface = take(4 * n), o_bmodel = take(4 * n), o_ql = take(32 * n),
-                 o_qd7 = take(4 * n), o_qi7 = take(4 * n), o_qpos = take(4 * n), o_qnb = take(4 * n),
-                 o_qnc = take(4 * n), o_pleaf = take(4 * n), o_pslot = take(4 * n), o_act0 = take(4 * n),
-                 o_act1 = take(4 * n), o_pend0 = take(4 * n), o_pend1 = take(4 * n), o_rw = take(4 * n),
-                 o_cnt0 = take(4 * nodes), o_cnt1 = take(4 * nodes), o_offs = take(4 * nodes),
-                 o_items = take(16 * (nodes + 64)), o_bucket = take(4 * n), o_ctl = take(sizeof(WFCtl));
-    HIPCHK(hipMalloc(&c->wf_mem.p, off));
-    c->wf_mem.n = off;
-    HIPCHK(hipMemset(c->wf_mem.p, 0, off));
-    char* b = static_cast<char*>(c->wf_mem.p);
-    WFParams& W = c->wf;
-    W.rng = reinterpret_cast<uint64_t*>(b + o_rng);
-    W.col = reinterpret_cast<float*>(b + o_col);
-    W.ret = reinterpret_cast<float*>(b + o_ret);
-    W.wt = reinterpret_cast<float*>(b + o_wt);
-    W.casts = reinterpret_cast<uint32_t*>(b + o_casts);
-    W.traced = reinterpret_cast<uint32_t*>(b + o_traced);
-    W.hface = reinterpret_cast<uint32_t*>(b + o_hface);
-    W.ht = reinterpret_cast<float*>(b + o_ht);
-    W.ro = reinterpret_cast<float*>(b + o_ro);
-    W.rd = reinterpret_cast<float*>(b + o_rd);
-    W.bt = reinterpret_cast<float*>(b + o_bt);
-    W.bu = reinterpret_cast<float*>(b + o_bu);
-    W.bv = reinterpret_cast<float*>(b + o_bv);
-    W.bface = reinterpret_cast<uint32_t*>(b + o_bface);
-    W.bmodel = reinterpret_cast<int32_t*>(b + o_bmodel);
-    W.ql = reinterpret_cast<int32_t*>(b + o_ql);
-    W.qd7 = reinterpret_cast<float*>(b + o_qd7);
-    W.qi7 = reinterpret_cast<int32_t*>(b + o_qi7);
-    W.qpos = reinterpret_cast<int32_t*>(b + o_qpos);
-    W.qnb = reinterpret_cast<int32_t*>(b + o_qnb);
-    W.qnc = reinterpret_cast<int32_t*>(b + o_qnc);
-    W.pleaf = reinterpret_cast<int32_t*>(b + o_pleaf);
-    W.pslot = reinterpret_cast<int32_t*>(b + o_pslot);
-    W.act[0] = reinterpret_cast<int32_t*>(b + o_act0);
-    W.act[1] = reinterpret_cast<int32_t*>(b + o_act1);
-    W.pend[0] = reinterpret_cast<int32_t*>(b + o_pend0);
-    W.pend[1] = reinterpret_cast<int32_t*>(b + o_pend1);
-    W.rw = reinterpret_cast<int32_t*>(b + o_rw);
-    W.cnt[0] = reinterpret_cast<uint32_t*>(b + o_cnt0);
-    W.cnt[1] = reinterpret_cast<uint32_t*>(b + o_cnt1);
-    W.offs = reinterpret_cast<int32_t*>(b + o_offs);
-    W.items = reinterpret_cast<int32_t*>(b + o_items);
-    W.bucket = reinterpret_cast<int32_t*>(b + o_bucket);
-    W.ctl = reinterpret_cast<WFCtl*>(b + o_ctl);
-    c->wf_n = n;
-    c->wf_nodes = nodes;
-    return ATR_OK;
-}
-
 void free_scene(atr_ctx* c) {
     for (DevBuf& b : c->scene_bufs) (void)hipFree(b.p);
     c->scene_bufs.clear();
@@ -435,26 +371,6 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
         if (hipMalloc(&b.dev_tiles.p, tneed) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
         b.dev_tiles.n = tneed;
     }
-    {   // pixel of every packed slot: a block's pixels occupy out_base.. in lane order (a cell
-        // plan's classes reorder the list, not the slots)
-        std::vector<int32_t> pix(size_t(b.packed_pixels > 0 ? b.packed_pixels : 1), 0);
-        for (const DBlock& blk : b.host) {
-            const uint64_t m = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
-            size_t k = size_t(blk.out_base);
-            for (int lane = 0; lane < 64; ++lane)
-                if ((m >> lane) & 1) pix[k++] = (blk.y0 + (lane >> 3)) * W + (blk.x0 + (lane & 7));
-        }
-        const size_t pneed = pix.size() * sizeof(int32_t);
-        if (b.dev_pix.n < pneed) {
-            if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
-            b.dev_pix = DevBuf();
-            if (hipMalloc(&b.dev_pix.p, pneed) != hipSuccess) { rc = ATR_E_NOMEM; return nullptr; }
-            b.dev_pix.n = pneed;
-        }
-        if (hipMemcpy(b.dev_pix.p, pix.data(), pneed, hipMemcpyHostToDevice) != hipSuccess) {
-            rc = ATR_E_NOMEM; b.width = -1; return nullptr;
-        }
-    }
     hipError_t e = hipMemcpy(b.dev.p, b.host.data(), b.host.size() * sizeof(DBlock), hipMemcpyHostToDevice);
     if (e == hipSuccess && ntiles)
         e = hipMemcpy(b.dev_tiles.p, tiles, sizeof(atr_tile) * size_t(ntiles), hipMemcpyHostToDevice);
@@ -474,28 +390,26 @@ int ensure_buf(DevBuf& d, size_t bytes, bool zero) {
 }
 
 // variant (atray.h) -> kernel schedule (render.hip). AUTO = the measured fastest.
+// variant (atray.h) -> schedule (render.hip / paths.hip); -1 = not a variant of this build.
 int sched_of(int32_t variant) {
     switch (variant) {
         case ATR_KERNEL_LANE: return 0;
-        case ATR_KERNEL_WAVE: return 1;
-        case ATR_KERNEL_TILE: return 2;
-        case ATR_KERNEL_TILE8: return 3;
-        case ATR_KERNEL_CLUSTER: return 4;
-        case ATR_KERNEL_PERSIST: return kSchedPersist;
         case ATR_KERNEL_FLAT: return 6;
         case ATR_KERNEL_HYBRID: return 7;
-        case ATR_KERNEL_AUTO: return 4;  // see auto_sched
-        default: return variant >= 16 ? variant : 0;
+        case ATR_KERNEL_PATHS: return kSchedPaths;
+        default: return -1;
     }
 }
 
 // AUTO: the fastest exact schedule for the camera (measured): primary-only renders
-// (bounce_limit 1, no AA) on HYBRID cells (lane-private leaf scans for coherent rays, dealt rounds
-// for the stragglers), everything else on the flattened cluster rounds (FLAT: incoherent
-// secondary rays diverge at every loop level).
+// (one sample, bounce_limit 1, no AA) on HYBRID cells (lane-private leaf scans for coherent rays,
+// dealt rounds for the stragglers); everything else on the sample-parallel path engine (a pixel's
+// samples side by side, one launch per bounce), or the FLAT cell megakernel for paths deeper than
+// its bounce launches.
 int auto_sched(int32_t variant, const atr_camera& cam) {
     if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
-    return cam.bounce_limit == 1 && !cam.anti_aliasing ? sched_of(ATR_KERNEL_HYBRID) : sched_of(ATR_KERNEL_FLAT);
+    if (cam.bounce_limit == 1 && !cam.anti_aliasing && cam.samples_per_pixel == 1) return sched_of(ATR_KERNEL_HYBRID);
+    return cam.bounce_limit <= kMaxPathBounces ? kSchedPaths : sched_of(ATR_KERNEL_FLAT);
 }
 
 // A single-frame launch of a cell schedule with the single-frame plan (tuning frame_plan, plan.hip):
@@ -510,7 +424,7 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
     const int32_t nb = int32_t(bs->host.size());
     // on top of a user cell plan too: its classes order the base list (and the multi-frame
     // launches), the frame plan re-orders that list for single frames by their measured cost
-    const bool use = c->tune.frame_plan && nb > 0 && sched != kSchedPersist &&
+    const bool use = c->tune.frame_plan && nb > 0 && sched != kSchedPaths &&
                      (!bs->plan_ready || bs->plan_stream == s);
     if (!use) {
         HIPCHK(launch_render(c, P, sched, s));
@@ -556,37 +470,116 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
     return ATR_OK;
 }
 
-// Launch a render schedule; PERSIST takes a zeroed set of queue heads from the ring first.
-hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
-    if (sched != kSchedPersist) {
-        if (!P.traced_rays) return atr_launch_render(P, sched, s);
-        // traced rays into a zeroed set of 64 spread counters, then one add to the caller's
-        const int k = c->tnext;
-        c->tnext = (k + 1) % kQueueSlots;
-        hipError_t e;
-        if (c->tused[k] && (e = hipStreamWaitEvent(s, c->tev[k], 0)) != hipSuccess) return e;
-        unsigned long long* caller = P.traced_rays;
-        P.traced_rays = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->tring) + size_t(k) * kTraceBytes);
-        e = atr_launch_render(P, sched, s);
-        if (e == hipSuccess) e = atr_launch_traced_finish(P.traced_rays, caller, s);
-        P.traced_rays = caller;
-        if (e != hipSuccess) return e;
-        if ((e = hipEventRecord(c->tev[k], s)) != hipSuccess) return e;
-        c->tused[k] = true;
-        return hipSuccess;
+// The path engine's workspace for stream s, at least `cap` paths per batch and `levels` bounce
+// levels. Growing waits for every launch of the context (the old buffers may still be read).
+hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, atr_ctx::PathWS*& out) {
+    atr_ctx::PathWS* ws = nullptr;
+    for (auto& w : c->path_ws)
+        if (w.stream == s) ws = &w;
+    if (!ws) {
+        c->path_ws.emplace_back();
+        ws = &c->path_ws.back();
+        ws->stream = s;
     }
+    if (ws->cap < cap || ws->levels < levels) {
+        hipError_t e;
+        if ((e = wait_all(c)) != hipSuccess) return e;
+        if (ws->mem.p && (e = hipFree(ws->mem.p)) != hipSuccess) return e;
+        ws->mem = DevBuf();
+        ws->cap = std::max(ws->cap, cap);
+        ws->levels = std::max(ws->levels, levels);
+        // 2 queues x kPathPlanes planes + the per-path results, 16 B per entry; the level counters
+        const size_t bytes = size_t(ws->cap) * 16 * (2 * kPathPlanes + 1) + size_t(ws->levels) * sizeof(PathCtl);
+        if ((e = hipMalloc(&ws->mem.p, bytes)) != hipSuccess) { ws->cap = 0; ws->levels = 0; return e; }
+        ws->mem.n = bytes;
+    }
+    out = ws;
+    return hipSuccess;
+}
+
+// The sample-parallel path engine (paths.hip) over a cell launch's blocks: the cell list in
+// batches of 2^tuning.path_batch_log2 paths, per batch the camera launch, one launch per further
+// bounce (persistent waves over the previous level's queue) and the per-pixel resolve, all on s.
+hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
+    const int64_t spp = P.cam.samples_per_pixel;
+    const int32_t bl = P.cam.bounce_limit;
     if (P.nblocks <= 0) return hipSuccess;
-    const int k = c->qnext;
-    c->qnext = (k + 1) % kQueueSlots;
-    uint32_t* q = reinterpret_cast<uint32_t*>(static_cast<char*>(c->qring) + size_t(k) * kQueueBytes);
+    if (bl > kMaxPathBounces) return hipErrorInvalidValue;
+    const int64_t per_cell = 64 * std::max<int64_t>(spp, 1);
+    const int64_t batch = std::max<int64_t>(1, (int64_t(1) << c->tune.path_batch_log2) / per_cell);
+    const int64_t cells = std::min<int64_t>(batch, P.nblocks);
+    const int32_t levels = std::max(bl, 1);
+    atr_ctx::PathWS* ws = nullptr;
     hipError_t e;
-    if (c->qused[k] && (e = hipStreamWaitEvent(s, c->qev[k], 0)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(q, 0, kQueueBytes, s)) != hipSuccess) return e;
-    P.queue = q;
-    P.qchunk = c->tune.persist_chunk;
-    if ((e = atr_launch_persist(P, c->ncu, s)) != hipSuccess) return e;
-    if ((e = hipEventRecord(c->qev[k], s)) != hipSuccess) return e;
-    c->qused[k] = true;
+    if ((e = path_workspace(c, s, cells * per_cell, levels, ws)) != hipSuccess) return e;
+    PathParams Q;
+    std::memset(&Q, 0, sizeof(Q));
+    Q.cam = P.cam;
+    Q.scene = P.scene;
+    Q.seed = P.seed;
+    Q.blocks = P.blocks;
+    Q.frame_blocks = P.frame_blocks;
+    Q.nblocks = P.nblocks;
+    Q.layout = P.layout;
+    Q.frame_stride = P.frame_stride;
+    Q.framebuffer = P.framebuffer;
+    Q.hit_face = P.hit_face;
+    Q.hit_t = P.hit_t;
+    Q.rgb = P.rgb;
+    Q.ray_casts = P.ray_casts;
+    Q.traced_rays = P.traced_rays;
+    Q.error_flag = P.error_flag;
+    Q.block_cost = P.block_cost;
+    Q.counters = P.counters;
+    float4_t* base = static_cast<float4_t*>(ws->mem.p);
+    Q.cap = ws->cap;
+    Q.q[0] = base;
+    Q.q[1] = base + kPathPlanes * ws->cap;
+    Q.out = base + 2 * kPathPlanes * ws->cap;
+    Q.ctl = reinterpret_cast<PathCtl*>(base + (2 * kPathPlanes + 1) * ws->cap);
+    Q.xcd_chunk = P.xcd_chunk;
+    Q.hyb_a = P.hyb_a;
+    Q.hyb_b = P.hyb_b;
+    Q.nfcam = P.nfcam;
+    for (int32_t f = 0; f < P.nfcam; ++f) Q.fcam[f] = P.fcam[f];
+    const int occ_cam = c->tune.path_camera_occ, occ_bounce = c->tune.path_bounce_occ;
+    for (int64_t c0 = 0; c0 < P.nblocks; c0 += cells) {
+        Q.cell0 = int32_t(c0);
+        Q.ncells = int32_t(std::min<int64_t>(cells, P.nblocks - c0));
+        if (bl > 0 && spp > 0) {
+            if ((e = hipMemsetAsync(Q.ctl, 0, sizeof(PathCtl) * size_t(levels), s)) != hipSuccess) return e;
+            if ((e = atr_launch_path_camera(Q, occ_cam, s)) != hipSuccess) return e;
+            for (int32_t k = 1; k < bl; ++k) {
+                Q.bounce = k;
+                if ((e = atr_launch_path_bounce(Q, c->ncu, occ_bounce, s)) != hipSuccess) return e;
+            }
+        }
+        if ((e = atr_launch_path_resolve(Q, s)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_kernels(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
+    if (sched == kSchedPaths) return launch_paths(c, P, s);
+    return atr_launch_render(P, sched, s);
+}
+
+// Launch a render schedule; the traced rays go into a zeroed set of 64 spread counters from the
+// ring, then one add to the caller's accumulator.
+hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
+    if (!P.traced_rays) return launch_kernels(c, P, sched, s);
+    const int k = c->tnext;
+    c->tnext = (k + 1) % kQueueSlots;
+    hipError_t e;
+    if (c->tused[k] && (e = hipStreamWaitEvent(s, c->tev[k], 0)) != hipSuccess) return e;
+    unsigned long long* caller = P.traced_rays;
+    P.traced_rays = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->tring) + size_t(k) * kTraceBytes);
+    e = launch_kernels(c, P, sched, s);
+    if (e == hipSuccess) e = atr_launch_traced_finish(P.traced_rays, caller, s);
+    P.traced_rays = caller;
+    if (e != hipSuccess) return e;
+    if ((e = hipEventRecord(c->tev[k], s)) != hipSuccess) return e;
+    c->tused[k] = true;
     return hipSuccess;
 }
 
@@ -849,9 +842,6 @@ int atr_create(int device, atr_ctx** out) {
         HIPCHK(hipMalloc(&c->d_error, 16));
         HIPCHK(hipMemset(c->d_error, 0, 16));
         HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
-        HIPCHK(hipMalloc(&c->qring, kQueueSlots * kQueueBytes));
-        HIPCHK(hipMemset(c->qring, 0, kQueueSlots * kQueueBytes));
-        for (hipEvent_t& e : c->qev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipMalloc(&c->tring, kQueueSlots * kTraceBytes));
         HIPCHK(hipMemset(c->tring, 0, kQueueSlots * kTraceBytes));
         for (hipEvent_t& e : c->tev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -873,8 +863,9 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
     if (!c || !t) return ATR_E_INVALID;
     if (t->xcd_chunk < 0 || t->xcd_chunk > 4096 || t->frame_rotate < 0 || t->frame_rotate > 1024 ||
         t->hybrid_a < -4096 || t->hybrid_a > 4096 || t->hybrid_b < -4096 || t->hybrid_b > 4096 ||
-        t->persist_chunk < 1 || t->persist_chunk > 4096 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
-        t->frame_plan < 0 || t->frame_plan > 1)
+        t->path_batch_log2 < 12 || t->path_batch_log2 > 30 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
+        t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
+        (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)))
         return ATR_E_INVALID;
     for (int32_t r : t->reserved)
         if (r) return ATR_E_INVALID;
@@ -896,22 +887,18 @@ int atr_destroy(atr_ctx* c) {
     for (BlockSet& b : c->blocks) {
         if (b.dev.p) (void)hipFree(b.dev.p);
         if (b.dev_tiles.p) (void)hipFree(b.dev_tiles.p);
-        if (b.dev_pix.p) (void)hipFree(b.dev_pix.p);
         if (b.dev_tile.p) (void)hipFree(b.dev_tile.p);
         for (DevBuf* d : {&b.cost, &b.cost_last, &b.plan_work, &b.plan_blocks})
             if (d->p) (void)hipFree(d->p);
         for (auto& se : b.evs) (void)hipEventDestroy(se.second);
     }
     for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
-    if (c->wf_mem.p) (void)hipFree(c->wf_mem.p);
-    if (c->wf_pinned) (void)hipHostFree(c->wf_pinned);
+    for (auto& w : c->path_ws)
+        if (w.mem.p) (void)hipFree(w.mem.p);
     if (c->d_error) (void)hipFree(c->d_error);
-    if (c->qring) (void)hipFree(c->qring);
     for (DevBuf& b : c->prog_blocks)
         if (b.p) (void)hipFree(b.p);
     for (hipEvent_t e : c->prog_ev)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->qev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
@@ -1177,11 +1164,6 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
         c->d_scene = static_cast<DScene*>(p);
     }
     c->nmodels = nmodels;
-    c->model_nodes.assign(size_t(nmodels), 1);
-    c->model_tree.assign(size_t(nmodels), 0);
-    for (int32_t i = 0; i < nmodels; ++i) {
-        if (models[i].tree) { c->model_nodes[size_t(i)] = models[i].tree->t.nnodes; c->model_tree[size_t(i)] = 1; }
-    }
     return ATR_OK;
 }
 
@@ -1238,36 +1220,8 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
     c->prog_active = false;
-    if (variant == ATR_KERNEL_WAVEFRONT) {
-        int64_t maxn = 1;
-        for (int32_t v : c->model_nodes) maxn = std::max<int64_t>(maxn, v);
-        if ((rc = wf_reserve(c, std::max<int64_t>(bs->packed_pixels, 1), maxn))) return rc;
-        if (!c->wf_pinned) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->wf_pinned), 64));
-        WFParams W = c->wf;
-        W.cam = *cam;
-        W.scene = c->d_scene;
-        W.seed = seed;
-        W.n = int32_t(bs->packed_pixels);
-        W.layout = fr->layout;
-        W.pix = static_cast<const int32_t*>(bs->dev_pix.p);
-        W.framebuffer = fr->framebuffer;
-        W.out_hit_face = fr->hit_face;
-        W.out_hit_t = fr->hit_t;
-        W.out_rgb = fr->rgb;
-        W.out_ray_casts = fr->ray_casts;
-        W.traced_rays = fr->traced_rays;
-        W.error_flag = c->d_error;
-        HIPCHK(hipEventRecord(c->ev_start, s));
-        if (W.n > 0)
-            HIPCHK(atr_wf_render(W, c->nmodels, c->model_nodes.data(), c->model_tree.data(), c->wf_pinned, s));
-        HIPCHK(hipEventRecord(c->ev_stop, s));
-        HIPCHK(hipEventRecord(c->ev_done, s));
-        HIPCHK(note_launch(c, s, bs));
-        c->have_render = true;
-        c->last_stream = s;
-        c->last_ntiles = ntiles;
-        return ATR_OK;
-    }
+    const int wave = auto_sched(variant, *cam);
+    if (wave < 0) return ATR_E_INVALID;
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1285,7 +1239,6 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.error_flag = c->d_error;
     P.counters = nullptr;
     apply_tuning(c, P);
-    const int wave = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     if ((rc = launch_planned(c, bs, P, wave, s))) return rc;
     HIPCHK(note_launch(c, s, bs));
@@ -1313,7 +1266,8 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
             return ATR_E_INVALID;
     }
     if (fr->layout != ATR_LAYOUT_IMAGE && fr->layout != ATR_LAYOUT_PACKED) return ATR_E_INVALID;
-    if (variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;
+    const int sched = auto_sched(variant, *cam);
+    if (sched < 0) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1340,15 +1294,14 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     apply_tuning(c, P);
-    const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     bool recorded = false;
-    if (sched != kSchedPersist && nframes == 1) {  // one frame: the single-frame plan applies
+    if (nframes == 1) {  // one frame: the single-frame plan applies
         P.nblocks = nb;
         P.frame_stride = frame_stride;
         if ((rc = launch_planned(c, bs, P, sched, s))) return rc;
         recorded = true;
-    } else if (sched != kSchedPersist) {  // one launch over frames x blocks (render_kernel: fidx)
+    } else {  // one launch over frames x blocks (render_kernel / paths: fidx)
         P.nblocks = nb * nframes;
         P.frame_blocks = nb;
         P.frame_stride = frame_stride;
@@ -1358,18 +1311,6 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
             for (int32_t f = 0; f < ncams; ++f) P.fcam[f] = cams[f];
         }
         HIPCHK(launch_render(c, P, sched, s));
-    } else {  // persistent lanes take pixels from a queue: one launch per frame
-        P.nblocks = nb;
-        for (int32_t f = 0; f < nframes; ++f) {
-            const size_t o = size_t(f) * size_t(frame_stride);
-            P.cam = cams[ncams > 1 ? f : 0];
-            P.framebuffer = fr->framebuffer + o;
-            P.hit_face = fr->hit_face ? fr->hit_face + o : nullptr;
-            P.hit_t = fr->hit_t ? fr->hit_t + o : nullptr;
-            P.rgb = fr->rgb ? fr->rgb + 3 * o : nullptr;
-            P.ray_casts = fr->ray_casts ? fr->ray_casts + o : nullptr;
-            HIPCHK(launch_render(c, P, sched, s));
-        }
     }
     if (!recorded) {
         HIPCHK(hipEventRecord(c->ev_stop, s));
@@ -1395,6 +1336,7 @@ int atr_render_start_cameras(atr_ctx* c, const atr_camera* cams, int32_t nframes
     return start_frames(c, cams, nframes, tiles, ntiles, fr, nframes, frame_stride, seed, stream, variant);
 }
 
+#ifdef ATR_DIAG
 int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                           uint64_t seed, int32_t variant, uint64_t* out, int64_t cap, int64_t* nblocks) {
     if (!c || !cam || !nblocks || ntiles < 0 || (ntiles && !tiles)) return ATR_E_INVALID;
@@ -1423,11 +1365,13 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.wave_trace = static_cast<unsigned long long*>(tr.p);
     apply_tuning(c, P);
     const int ts = sched_of(variant);  // per-cell trace: 8x8-cell schedules only
-    HIPCHK(atr_launch_render(P, ts == kSchedPersist ? 4 : ts, nullptr));
+    HIPCHK(atr_launch_render(P, ts < 0 || ts == kSchedPaths ? 7 : ts, nullptr));
     HIPCHK(hipDeviceSynchronize());
     if (nb) HIPCHK(hipMemcpy(out, tr.p, 3 * nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;
 }
+
+#endif  // ATR_DIAG
 
 // One instrumented (COUNT) render; h = the 16 device counters (render.hip: [0..9] work counters,
 // [10..15] phase clocks, zero unless built with -DATR_PHASE_CLOCKS).
@@ -1458,9 +1402,8 @@ static int count_launch(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     P.counters = static_cast<unsigned long long*>(ctr.p);
     apply_tuning(c, P);  // the product's HYBRID thresholds (the counts do not depend on them, the clocks do)
     const int sc = auto_sched(variant, *cam);
-    // diagnostic codes: the CC schedules (96+) have COUNT builds; other occupancy variants count
-    // with their base schedule
-    HIPCHK(launch_render(c, P, sc >= 96 ? sc : (sc >= 32 ? 4 : (sc >= 16 ? 0 : sc)), nullptr));
+    if (sc < 0) return ATR_E_INVALID;
+    HIPCHK(launch_render(c, P, sc, nullptr));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h, ctr.p, kCounterSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;
@@ -1476,6 +1419,7 @@ int atr_render_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     return ATR_OK;
 }
 
+#ifdef ATR_DIAG
 int atr_render_phase_clocks(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                             uint64_t seed, int32_t variant, int64_t out[6]) {
     if (!out) return ATR_E_INVALID;
@@ -1509,6 +1453,8 @@ int atr_render_simd_counters(atr_ctx* c, const atr_camera* cam, const atr_tile* 
     return ATR_OK;
 }
 
+#endif  // ATR_DIAG
+
 int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                           uint64_t seed, int64_t* cost_out) {
     if (!c || !cam || (ntiles && (!tiles || !cost_out)) || ntiles < 0) return ATR_E_INVALID;
@@ -1535,7 +1481,7 @@ int atr_render_tile_costs(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost.p);
     apply_tuning(c, P);
-    HIPCHK(atr_launch_render(P, auto_sched(ATR_KERNEL_AUTO, *cam), nullptr));  // per-cell clocks, AUTO's kernel
+    HIPCHK(launch_render(c, P, auto_sched(ATR_KERNEL_AUTO, *cam), nullptr));  // per-cell clocks, AUTO's kernels
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
     if (nb) HIPCHK(hipMemcpy(h.data(), cost.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -1568,7 +1514,7 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
     if (!c || !cam || !fr || !fr->framebuffer || ntiles < 0 || (ntiles && !tiles) || tiles_per_launch < 1)
         return ATR_E_INVALID;
     if (cam->width <= 0 || cam->height <= 0 || cam->width > (1 << 16) || cam->height > (1 << 16)) return ATR_E_INVALID;
-    if (fr->layout != ATR_LAYOUT_IMAGE || variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;
+    if (fr->layout != ATR_LAYOUT_IMAGE) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1847,9 +1793,9 @@ int atr_render_cell_costs(atr_ctx* c, const atr_camera* cam, uint64_t seed, int3
     P.error_flag = c->d_error;
     P.block_cost = static_cast<unsigned long long*>(cost.p);
     apply_tuning(c, P);
-    if (variant == ATR_KERNEL_PERSIST || variant == ATR_KERNEL_WAVEFRONT) return ATR_E_INVALID;  // cell kernels only
     const int sched = auto_sched(variant, *cam);
-    HIPCHK(atr_launch_render(P, sched, nullptr));
+    if (sched < 0) return ATR_E_INVALID;
+    HIPCHK(launch_render(c, P, sched, nullptr));
     HIPCHK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nb);
     if (nb) HIPCHK(hipMemcpy(h.data(), cost.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));

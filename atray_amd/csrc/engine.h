@@ -68,9 +68,12 @@ ATR_HD float rand_bi(uint64_t& state, uint64_t stream) {  // PL_math.h:525-541
     float rd = (float)pcg_next(state, stream) * kInvU32Max;
     return -1.0f + 2.0f * rd;
 }
-// Per-pixel stream (deviation from renderer.cpp:376-378's rdtsc*thread seeding).
-ATR_HD void pixel_stream(uint64_t seed, int64_t pixel, uint64_t& state, uint64_t& stream) {
-    uint64_t x = seed ^ (uint64_t)pixel;
+// One PCG stream per (pixel, sample) (deviation from renderer.cpp:376-378's rdtsc*thread seeding,
+// DESIGN.md §2): state = splitmix64(seed ^ pixel ^ sample << 40), increment 2 pixel + 1. A pixel's
+// samples are independent paths, so they can run in parallel (paths.hip); sample 0's stream is the
+// round-1..3 per-pixel stream.
+ATR_HD void path_stream(uint64_t seed, int64_t pixel, uint32_t sample, uint64_t& state, uint64_t& stream) {
+    uint64_t x = seed ^ (uint64_t)pixel ^ ((uint64_t)sample << 40);
     x += 0x9E3779B97F4A7C15ULL;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
@@ -191,13 +194,57 @@ struct RenderParams {
     unsigned long long* block_cost;  // non-null -> shader clocks added per base block (blocks[b].base)
     unsigned long long* wave_trace;  // non-null -> per block: start, end (100 MHz clock), HW_ID | XCC_ID << 32
     int32_t xcd_chunk;  // 0: contiguous block range per XCD; k > 0: k-workgroup chunks dealt round-robin
-    uint32_t* queue;    // PERSIST: 8 zeroed per-XCD work-queue heads (persist.hip)
-    int32_t qchunk;     // PERSIST: 8x8 cells per queue chunk
     int32_t frame_blocks;  // > 0: nblocks = frames x frame_blocks, one launch renders every frame
     int64_t frame_stride;  // output elements between consecutive frames (rgb: 3 x this)
     int32_t frame_rotate;  // frame f's blocks start f / frames x frame_rotate / 1024 into its list
     int32_t hyb_a, hyb_b;  // HYBRID: a step's leaves are dealt in rounds when max clusters > a x rounds + b
     int32_t nfcam;         // > 0: frame f renders with fcam[f] instead of cam (same size/spp/bounces)
+    atr_camera fcam[kMaxFrameCams];
+};
+
+// Sample-parallel path engine (paths.hip): one lane per (pixel, sample) path. A batch
+// is a contiguous range [cell0, cell0 + ncells) of the launch's cell list (frames interleaved as in
+// RenderParams: cell c renders block c / nf of frame c % nf); its paths are numbered
+// g = (c - cell0) x 64 spp + pixel lane x spp + sample, so every wavefront of 64 consecutive paths
+// lies in one cell. Path records between bounces are four float4 planes of `cap` entries each:
+//   p0 = {o.xyz, d.x}, p1 = {d.y, d.z, bits(pixel), bits(g)}, p2 = {ret.xyz, w.x},
+//   p3 = {w.y, w.z, bits(rng lo), bits(rng hi)};
+// a finished path leaves {colour.xyz, bits(ray_casts)} in out[g].
+constexpr int kPathPlanes = 4;
+// Per bounce level k of a batch (zeroed before the batch): the launch of level k (0 = the camera
+// rays) appends its surviving paths to queue k & 1 (tail); the bounce launch k + 1 reads them,
+// its persistent waves claiming 64 at a time (head of level k + 1).
+struct PathCtl {
+    uint32_t tail;
+    uint32_t head;
+};
+struct PathParams {
+    atr_camera cam;
+    const DScene* scene;
+    uint64_t seed;
+    const DBlock* blocks;
+    int32_t frame_blocks;  // blocks per frame (the launch's frames: nf = nblocks / frame_blocks)
+    int32_t nblocks;       // cells of the launch (all frames)
+    int32_t cell0, ncells; // this batch
+    int32_t layout;
+    int64_t frame_stride;
+    uint32_t* framebuffer;
+    uint32_t* hit_face;
+    float* hit_t;
+    float* rgb;
+    uint32_t* ray_casts;
+    unsigned long long* traced_rays;  // 64 spread counters (a ring slot), or null
+    int32_t* error_flag;
+    unsigned long long* block_cost;   // non-null -> shader clocks per base block (calibration)
+    float4_t* q[2];   // path queues, kPathPlanes planes of cap entries each
+    int64_t cap;      // entries per plane (>= the batch's paths)
+    float4_t* out;    // per path: colour and ray_casts of the finished path
+    PathCtl* ctl;     // one per bounce level
+    unsigned long long* counters;  // non-null -> instrumented kernels (counters [0..9] of render.hip)
+    int32_t bounce;   // bounce launch: this bounce (1 .. bounce_limit - 1)
+    int32_t xcd_chunk;
+    int32_t hyb_a, hyb_b;
+    int32_t nfcam;
     atr_camera fcam[kMaxFrameCams];
 };
 

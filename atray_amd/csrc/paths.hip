@@ -1,0 +1,303 @@
+// paths.hip -- the sample-parallel path engine for multi-bounce renders.
+//
+// render_tile_from_camera (renderer.cpp:336-358) runs a pixel's spp samples one after another,
+// each a cast_ray bounce loop (:213-262). With one PCG stream per (pixel, sample) (engine.h
+// path_stream) the samples are independent paths, so here every lane owns one PATH and a pixel's
+// samples run side by side:
+//   path_camera_kernel  one wavefront = 64 consecutive paths of one 8x8 cell (a pixel's samples
+//                       together): the camera rays (one origin per wave: HYBRID's coherent flavour,
+//                       scan.h), then the first shading step; a path that goes on is appended to a
+//                       queue (a ballot, one atomic per wave);
+//   path_bounce_kernel  bounce k of every queued path: persistent waves claim 64 queue entries at a
+//                       time, trace them (FLAT's dealt rounds for incoherent rays), shade, and
+//                       append the survivors to the other queue -- one launch per bounce level, so
+//                       the trace holds no path state (loaded after the query) and each kernel has
+//                       its own register budget;
+//   path_resolve_kernel per pixel, the sample colours summed in sample order with the reference's
+//                       f32 adds (col += cast_ray(...), :353-356), then average, clamp, BGRX byte
+//                       conversion (:358-365) -- every output bit-identical to the cell kernels'.
+// A batch is a range of the launch's cell list (PathParams, engine.h); the host runs camera,
+// bounces and resolve per batch on one stream (capi.cpp launch_paths).
+#include <hip/hip_runtime.h>
+
+#include "scan.h"
+
+namespace atr {
+
+// (The helpers take plain values: a reference to the kernel argument passed to a function made the
+// compiler copy the whole 1.8-KB argument into scratch.)
+// cell c of the launch's list -> its frame and block (frames interleaved, RenderParams)
+__device__ __forceinline__ void cell_of(int32_t frame_blocks, int32_t nblocks, int32_t c, int32_t& fidx, int32_t& bi) {
+    const int32_t nf = frame_blocks > 0 ? nblocks / frame_blocks : 1;
+    fidx = c % nf;
+    bi = c / nf;
+}
+
+__device__ __forceinline__ size_t out_index(int32_t layout, int32_t width, int64_t frame_stride, const DBlock& blk,
+                                            uint64_t mask, int pl, int32_t fidx) {
+    size_t o;
+    if (layout == ATR_LAYOUT_PACKED) o = size_t(blk.out_base) + __popcll(mask & ((uint64_t(1) << pl) - 1));
+    else o = size_t(blk.y0 + (pl >> 3)) * size_t(width) + size_t(blk.x0 + (pl & 7));
+    return o + size_t(fidx) * size_t(frame_stride);
+}
+
+// A finished path: its colour (cast_ray's ret) and the reference's ray_casts (renderer.cpp:260).
+__device__ __forceinline__ void path_finish(float4_t* out, int64_t g, V3 ret, uint32_t casts) {
+    out[g] = float4_t{ret.x, ret.y, ret.z, __uint_as_float(casts)};
+}
+
+// Append this lane's path (if `go`) to queue q (planes `cap` entries apart): one atomic per wave for
+// the wave's survivors, each at base + its rank among them.
+__device__ __forceinline__ void path_enqueue(float4_t* q, int64_t cap, PathCtl* ctl, bool go, V3 o, V3 d,
+                                             uint32_t pix, uint32_t g, V3 ret, V3 w, uint64_t st) {
+    const uint64_t m = __ballot(go);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&ctl->tail, uint32_t(__popcll(m)));
+    base = uint32_t(__builtin_amdgcn_readfirstlane(int(__shfl(int(base), 0))));
+    if (!go) return;
+    const int64_t e = int64_t(base) + __popcll(m & ((uint64_t(1) << lane) - 1));
+    q[e] = float4_t{o.x, o.y, o.z, d.x};
+    q[cap + e] = float4_t{d.y, d.z, __uint_as_float(pix), __uint_as_float(g)};
+    q[2 * cap + e] = float4_t{ret.x, ret.y, ret.z, w.x};
+    q[3 * cap + e] = float4_t{w.y, w.z, __uint_as_float(uint32_t(st)), __uint_as_float(uint32_t(st >> 32))};
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void path_counters(unsigned long long* C, const Ctr& ct, uint32_t traced) {
+    const int lane = threadIdx.x & 63;
+    uint32_t v[10] = {traced, ct.box, ct.tri, ct.leaf, ct.wave_tri, ct.pass, ct.box_all, 0u, ct.cbox, ct.screen};
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint32_t t = v[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if (lane == 0 && t) atomicAdd(C + k, (unsigned long long)t);
+    }
+    if (lane == 0) atomicAdd(C + 7, 1ull);
+}
+
+// ------------------------------------------------------------------ camera rays + first shading
+template <bool COUNT, int OCC>
+__global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const uint32_t spp = uint32_t(__builtin_amdgcn_readfirstlane(int(P.cam.samples_per_pixel)));
+    const int64_t wv = int64_t(remap_xcd(blockIdx.x, gridDim.x, P.xcd_chunk)) * 4 + wave;  // wave of the batch
+    if (wv >= int64_t(P.ncells) * spp) return;  // whole wavefront
+    // a cell's 64 x spp paths are spp consecutive waves: the cell is wave-uniform
+    const int32_t cellrel = int32_t(wv / spp);
+    const uint32_t r = uint32_t(wv - int64_t(cellrel) * spp) * 64u + uint32_t(lane);  // path within the cell
+    const int pl = int(r / spp);  // the pixel's lane in the 8x8 cell
+    const uint32_t s = r - uint32_t(pl) * spp;  // its sample
+    const int64_t g = int64_t(cellrel) * 64 * spp + r;
+    int32_t fidx, bi;
+    cell_of(P.frame_blocks, P.nblocks, P.cell0 + cellrel, fidx, bi);
+    const DBlock blk = P.blocks[bi];
+    const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+    const atr_camera& cm = P.nfcam > 0 ? P.fcam[__builtin_amdgcn_readfirstlane(fidx)] : P.cam;
+    const int32_t bl = cm.bounce_limit;
+    const bool active = ((mask >> pl) & 1) && bl > 0;
+    const uint64_t clk0 = P.block_cost ? clock64() : 0;
+    const DScene* S = uniform_global(P.scene);
+    const int32_t x = blk.x0 + (pl & 7), y = blk.y0 + (pl >> 3);
+    const int64_t pix = int64_t(y) * cm.width + x;
+    uint64_t st, stream;
+    path_stream(P.seed, pix, s, st, stream);
+    const float film_y = -1.0f + 2.0f * (float(y) / float(cm.height));                                  // :317
+    const float film_x = ((-1.0f + 2.0f * (float(x) / float(cm.width))) * cm.h_fov) * cm.aspect_ratio;  // :329
+    const V3 eye = from(cm.eye), fc = from(cm.frame_center), cx = from(cm.camera_x), cy = from(cm.camera_y);
+    V3 d;
+    if (cm.anti_aliasing) {  // :338-347, the sample's two jitter draws
+        const float xo = rand_bi(st, stream) * cm.half_pixel_width + film_x;
+        const float yo = rand_bi(st, stream) * cm.half_pixel_height + film_y;
+        d = unit(sub(add(add(fc, scale(cx, xo)), scale(cy, yo)), eye));
+    } else {
+        d = unit(sub(add(add(fc, scale(cx, film_x)), scale(cy, film_y)), eye));  // :350-351
+    }
+    int err = 0;
+    Ctr ct;
+    Isect id;
+    id.type = T_NONE;
+    intersect_scene<SCHED_HYBRID, FLAV_CAMERA, COUNT>(S, eye, d, active, id, err, ct, P.hyb_a, P.hyb_b);
+    bool go = false;
+    V3 o = eye, ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
+    if (active) {
+        if (s == 0) {  // sample 0's camera ray: the primary hit outputs
+            const size_t oi = out_index(P.layout, cm.width, P.frame_stride, blk, mask, pl, fidx);
+            if (P.hit_face) P.hit_face[oi] = id.face;
+            if (P.hit_t) P.hit_t[oi] = id.t;
+        }
+        const DMaterial& mat = S->mats[id.material];
+        if (id.type == T_SKY) {  // :225-229 at i = 0
+            ret = add(ret, had(w, mk(mat.ex, mat.ey, mat.ez)));
+            path_finish(P.out, g, ret, 0u);
+        } else {
+            bounce_shade(mat, id, o, d, ret, w, st, stream);  // :231-258
+            if (bl <= 1) path_finish(P.out, g, ret, uint32_t(bl));  // ran to the limit (:260)
+            else go = true;
+        }
+    }
+    path_enqueue(P.q[0], P.cap, &P.ctl[0], go, o, d, uint32_t(pix), uint32_t(g), ret, w, st);
+    const uint32_t traced = active ? 1u : 0u;
+    if (P.traced_rays) add_traced(P.traced_rays, traced, int(wv));
+    if (err && P.error_flag) atomicOr(P.error_flag, 1);
+    if (P.block_cost && lane == 0) atomicAdd(P.block_cost + blk.base, (unsigned long long)(clock64() - clk0));
+    if constexpr (COUNT) path_counters<COUNT>(P.counters, ct, traced);
+}
+
+// ------------------------------------------------------------------ bounce k of the queued paths
+template <bool COUNT, int OCC>
+__global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
+    const int lane = threadIdx.x & 63;
+    const int32_t k = P.bounce;  // 1 .. bounce_limit - 1
+    const int32_t bl = P.cam.bounce_limit;
+    const float4_t* __restrict__ qin = P.q[(k - 1) & 1];
+    const uint32_t n = uint32_t(__builtin_amdgcn_readfirstlane(int(P.ctl[k - 1].tail)));
+    const DScene* S = uniform_global(P.scene);
+    const uint32_t spp = P.cam.samples_per_pixel;
+    int err = 0;
+    Ctr ct;
+    uint32_t traced = 0;
+    for (;;) {  // every wave leaves once the queue is claimed: the exit every wave reaches
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&P.ctl[k].head, 64u);
+        base = uint32_t(__builtin_amdgcn_readfirstlane(int(__shfl(int(base), 0))));
+        if (base >= n) break;
+        const uint64_t clk0 = P.block_cost ? clock64() : 0;
+        const uint32_t e = base + uint32_t(lane);
+        const bool valid = e < n;
+        V3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
+        if (valid) {
+            const float4_t a = qin[e], b = qin[P.cap + e];
+            o = mk(a.x, a.y, a.z);
+            d = mk(a.w, b.x, b.y);
+        }
+        Isect id;
+        id.type = T_NONE;
+        intersect_scene<SCHED_FLAT, FLAV_BOUNCE, COUNT>(S, o, d, valid, id, err, ct, P.hyb_a, P.hyb_b);
+        __asm__ volatile("" ::: "memory");  // the path state is read after the query, not held through it
+        bool go = false;
+        uint32_t pix = 0, g = 0;
+        V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
+        uint64_t st = 0;
+        if (valid) {
+            traced += 1;
+            const float4_t b = qin[P.cap + e], c = qin[2 * P.cap + e], q3 = qin[3 * P.cap + e];
+            pix = __float_as_uint(b.z);
+            g = __float_as_uint(b.w);
+            ret = mk(c.x, c.y, c.z);
+            w = mk(c.w, q3.x, q3.y);
+            st = uint64_t(__float_as_uint(q3.z)) | (uint64_t(__float_as_uint(q3.w)) << 32);
+            const uint64_t stream = (uint64_t(pix) << 1) | 1ULL;
+            const DMaterial& mat = S->mats[id.material];
+            if (id.type == T_SKY) {  // :225-229 at i = k
+                ret = add(ret, had(w, mk(mat.ex, mat.ey, mat.ez)));
+                path_finish(P.out, g, ret, uint32_t(k));
+            } else {
+                bounce_shade(mat, id, o, d, ret, w, st, stream);  // :231-258
+                if (k + 1 >= bl) path_finish(P.out, g, ret, uint32_t(bl));  // ran to the limit (:260)
+                else go = true;
+            }
+            if (P.block_cost) {  // calibration: the chunk's clocks split over its paths' cells
+                const int32_t c = P.cell0 + int32_t(g / (64u * spp));
+                int32_t fidx, bi;
+                cell_of(P.frame_blocks, P.nblocks, c, fidx, bi);
+                const uint32_t nv = n - base < 64u ? n - base : 64u;
+                atomicAdd(P.block_cost + P.blocks[bi].base, (unsigned long long)((clock64() - clk0) / nv));
+            }
+        }
+        path_enqueue(P.q[k & 1], P.cap, &P.ctl[k], go, o, d, pix, g, ret, w, st);
+    }
+    if (P.traced_rays) add_traced(P.traced_rays, traced, int(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (err && P.error_flag) atomicOr(P.error_flag, 1);
+    if constexpr (COUNT) path_counters<COUNT>(P.counters, ct, traced);
+}
+
+// ------------------------------------------------------------------ per-pixel resolve
+__global__ __launch_bounds__(256) void path_resolve_kernel(PathParams P) {
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const int32_t cellrel = int32_t(blockIdx.x) * 4 + wave;
+    if (cellrel >= P.ncells) return;
+    int32_t fidx, bi;
+    cell_of(P.frame_blocks, P.nblocks, P.cell0 + cellrel, fidx, bi);
+    const DBlock blk = P.blocks[bi];
+    const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+    if (!((mask >> lane) & 1)) return;
+    const atr_camera& cm = P.nfcam > 0 ? P.fcam[__builtin_amdgcn_readfirstlane(fidx)] : P.cam;
+    const uint32_t spp = cm.samples_per_pixel;
+    const bool traced = cm.bounce_limit > 0;
+    const float4_t* src = P.out + (int64_t(cellrel) * 64 + lane) * int64_t(spp);
+    V3 col = mk(0.f, 0.f, 0.f);
+    uint32_t casts = 0;
+    for (uint32_t s = 0; s < spp; ++s) {  // col += cast_ray(...) in sample order (:353-356)
+        V3 c = mk(0.f, 0.f, 0.f);
+        if (traced) {
+            const float4_t v = src[s];
+            c = mk(v.x, v.y, v.z);
+            casts += __float_as_uint(v.w);
+        }
+        col = add(col, c);
+    }
+    col = divs(col, float(spp));  // :358
+    const float cr = pl_max(0.0f, pl_min(col.x, 1.0f));
+    const float cg = pl_max(0.0f, pl_min(col.y, 1.0f));
+    const float cb = pl_max(0.0f, pl_min(col.z, 1.0f));
+    const uint32_t r8 = uint32_t(cr * 255.0f) & 0xFFu, g8 = uint32_t(cg * 255.0f) & 0xFFu,
+                   b8 = uint32_t(cb * 255.0f) & 0xFFu;
+    const size_t o = out_index(P.layout, cm.width, P.frame_stride, blk, mask, lane, fidx);
+    P.framebuffer[o] = b8 | (g8 << 8) | (r8 << 16);  // Set_Pixel (texture.h:27-38)
+    if (!traced || spp == 0) {  // no camera ray ran: the miss record
+        if (P.hit_face) P.hit_face[o] = 0xFFFFFFFFu;
+        if (P.hit_t) P.hit_t[o] = kMaxFloat;
+    }
+    if (P.rgb) { P.rgb[3 * o] = col.x; P.rgb[3 * o + 1] = col.y; P.rgb[3 * o + 2] = col.z; }
+    if (P.ray_casts) P.ray_casts[o] = casts;
+}
+
+// Occupancy (waves/SIMD) of the two trace kernels, 5..7 (the LDS limit is 7: 22.5 KB per
+// workgroup); tuning path_camera_occ / path_bounce_occ pick another (0 = these defaults).
+constexpr int kCameraOcc = 7;
+constexpr int kBounceOcc = 7;
+template __global__ void path_camera_kernel<false, 5>(PathParams);
+template __global__ void path_camera_kernel<false, 6>(PathParams);
+template __global__ void path_camera_kernel<false, 7>(PathParams);
+template __global__ void path_camera_kernel<true, 4>(PathParams);
+template __global__ void path_bounce_kernel<false, 5>(PathParams);
+template __global__ void path_bounce_kernel<false, 6>(PathParams);
+template __global__ void path_bounce_kernel<false, 7>(PathParams);
+template __global__ void path_bounce_kernel<true, 4>(PathParams);
+
+}  // namespace atr
+
+// ------------------------------------------------------------------ launchers used by capi.cpp
+extern "C" hipError_t atr_launch_path_camera(const atr::PathParams& P, int occ, hipStream_t s) {
+    const int64_t waves = int64_t(P.ncells) * P.cam.samples_per_pixel;
+    if (waves <= 0) return hipSuccess;
+    const dim3 g(unsigned((waves + 3) / 4)), b(256);
+    if (!occ) occ = atr::kCameraOcc;
+    if (P.counters) hipLaunchKernelGGL((atr::path_camera_kernel<true, 4>), g, b, 0, s, P);
+    else if (occ == 5) hipLaunchKernelGGL((atr::path_camera_kernel<false, 5>), g, b, 0, s, P);
+    else if (occ == 6) hipLaunchKernelGGL((atr::path_camera_kernel<false, 6>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((atr::path_camera_kernel<false, 7>), g, b, 0, s, P);
+    return hipGetLastError();
+}
+
+// Persistent: `ncu` x occupancy workgroups (4 waves each, one per SIMD) claim the queue 64 entries
+// at a time.
+extern "C" hipError_t atr_launch_path_bounce(const atr::PathParams& P, int ncu, int occ, hipStream_t s) {
+    const dim3 b(256);
+    if (!occ) occ = atr::kBounceOcc;
+    const dim3 g(unsigned(ncu) * unsigned(P.counters ? 4 : occ));
+    if (P.counters) hipLaunchKernelGGL((atr::path_bounce_kernel<true, 4>), g, b, 0, s, P);
+    else if (occ == 5) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 5>), g, b, 0, s, P);
+    else if (occ == 6) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 6>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((atr::path_bounce_kernel<false, 7>), g, b, 0, s, P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t atr_launch_path_resolve(const atr::PathParams& P, hipStream_t s) {
+    if (P.ncells <= 0) return hipSuccess;
+    hipLaunchKernelGGL(atr::path_resolve_kernel, dim3(unsigned((P.ncells + 3) / 4)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}

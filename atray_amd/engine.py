@@ -25,12 +25,12 @@ ATR_PLAN_PRIO = 0x80  # cell plan: raised issue priority (atr_set_cell_plan)
 def plan_class(c):
     """Cell plan dispatch class (ATR_PLAN_CLASS): class 7 cells are dispatched first, class 0 last."""
     return (int(c) & 7) << 4
-ATR_KERNEL_AUTO, ATR_KERNEL_LANE, ATR_KERNEL_WAVE, ATR_KERNEL_TILE, ATR_KERNEL_TILE8 = 0, 1, 2, 3, 4
-ATR_KERNEL_WAVEFRONT = 5
-ATR_KERNEL_CLUSTER = 6
-ATR_KERNEL_PERSIST = 7
+ATR_KERNEL_AUTO, ATR_KERNEL_LANE = 0, 1
 ATR_KERNEL_FLAT = 8
 ATR_KERNEL_HYBRID = 9
+ATR_KERNEL_PATHS = 10
+# the kernel variants of the shipping library (atray.h); AUTO picks HYBRID or PATHS
+VARIANTS = (ATR_KERNEL_LANE, ATR_KERNEL_FLAT, ATR_KERNEL_HYBRID, ATR_KERNEL_PATHS)
 MISS = 0xFFFFFFFF
 MAX_FLOAT = np.float32(3.402823466e38)
 
@@ -92,8 +92,9 @@ class atr_frame(C.Structure):
 
 class atr_tuning(C.Structure):
     _fields_ = [("xcd_chunk", C.c_int32), ("frame_rotate", C.c_int32), ("hybrid_a", C.c_int32),
-                ("hybrid_b", C.c_int32), ("persist_chunk", C.c_int32), ("cluster_size", C.c_int32),
-                ("frame_plan", C.c_int32), ("reserved", C.c_int32 * 5)]
+                ("hybrid_b", C.c_int32), ("path_batch_log2", C.c_int32), ("cluster_size", C.c_int32),
+                ("frame_plan", C.c_int32), ("path_camera_occ", C.c_int32), ("path_bounce_occ", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 # every symbol include/atray.h declares (checked by tests/test_capi_symbols.py)
@@ -103,16 +104,18 @@ EXPORTS = [
     "atr_octree_from_nodes", "atr_octree_free", "atr_octree_export", "atr_octree_stats", "atr_camera_set",
     "atr_make_tiles", "atr_make_shard_tiles", "atr_create", "atr_destroy", "atr_version",
     "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
-    "atr_render_counters", "atr_render_tile_costs", "atr_render_wave_trace", "atr_balance_shard_tiles",
+    "atr_render_counters", "atr_render_tile_costs", "atr_balance_shard_tiles",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
     "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
-    "atr_render_phase_clocks", "atr_render_path_counters", "atr_default_tuning", "atr_set_tuning",
-    "atr_get_tuning", "atr_render_simd_counters", "atr_pack_bgr", "atr_scatter_bgr",
+    "atr_default_tuning", "atr_set_tuning", "atr_get_tuning", "atr_pack_bgr", "atr_scatter_bgr",
     "atr_render_plan_info",
 ]
+# the diagnostic build's extra symbols (include/atray_diag.h; make -C atray_amd/csrc DIAG=1)
+DIAG_EXPORTS = ["atr_render_wave_trace", "atr_render_phase_clocks", "atr_render_path_counters",
+                "atr_render_simd_counters"]
 
 _lib = None
 
@@ -188,6 +191,8 @@ def lib():
         "atr_memcpy_d2h": ([vp, vp, vp, C.c_size_t], C.c_int),
         "atr_memset_d": ([vp, vp, C.c_int, C.c_size_t], C.c_int),
     }
+    for name in [n for n in DIAG_EXPORTS if not hasattr(L, n)]:
+        del sig[name]  # product build: the diagnostic entry points are absent
     for name, (args, res) in sig.items():
         f = getattr(L, name)
         f.argtypes = args

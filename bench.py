@@ -241,12 +241,12 @@ def main():
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "wave", "tile", "tile8", "wf", "cl", "ps", "flat", "hyb"])
+    ap.add_argument("--variant", default="auto", choices=["auto", "lane", "flat", "hyb", "paths"])
     ap.add_argument("--variant-code", type=int, default=-1,
                     help="diagnostic: raw kernel code passed to the engine (overrides --variant's kernel)")
     ap.add_argument("--tuning", default="",
                     help="diagnostic: k=v,... scheduling knobs for atr_set_tuning (xcd_chunk, frame_rotate, hybrid_a, "
-                         "hybrid_b, persist_chunk, cluster_size); outputs never change")
+                         "hybrid_b, path_batch_log2, cluster_size, path_camera_occ, path_bounce_occ); outputs never change")
     ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -415,12 +415,10 @@ def run(args):
             dist.init_process_group(backend)
 
     asset, W, H, spp, bounces, use_tree = CONFIGS[args.config]
-    variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "wave": E.ATR_KERNEL_WAVE,
-               "tile": E.ATR_KERNEL_TILE, "tile8": E.ATR_KERNEL_TILE8,
-               "wf": E.ATR_KERNEL_WAVEFRONT, "cl": E.ATR_KERNEL_CLUSTER,
-               "ps": E.ATR_KERNEL_PERSIST, "flat": E.ATR_KERNEL_FLAT, "hyb": E.ATR_KERNEL_HYBRID}[args.variant]
-    VARIANT_NAMES.update({E.ATR_KERNEL_AUTO: "auto", E.ATR_KERNEL_CLUSTER: "cluster", E.ATR_KERNEL_FLAT: "flat",
-                          E.ATR_KERNEL_HYBRID: "hybrid", E.ATR_KERNEL_PERSIST: "persist", E.ATR_KERNEL_LANE: "lane"})
+    variant = {"auto": E.ATR_KERNEL_AUTO, "lane": E.ATR_KERNEL_LANE, "flat": E.ATR_KERNEL_FLAT,
+               "hyb": E.ATR_KERNEL_HYBRID, "paths": E.ATR_KERNEL_PATHS}[args.variant]
+    VARIANT_NAMES.update({E.ATR_KERNEL_AUTO: "auto", E.ATR_KERNEL_FLAT: "flat", E.ATR_KERNEL_HYBRID: "hybrid",
+                          E.ATR_KERNEL_LANE: "lane", E.ATR_KERNEL_PATHS: "paths"})
     if args.variant_code >= 0:
         variant = args.variant_code
     # ---- scene prep (untimed for Mrays/s; reported under "prep")
@@ -724,10 +722,10 @@ def run(args):
         casts_frames = sum(nf for _, nf in last.values())
 
     # ---- the roofline kernel: the timed launches' schedule, one app-camera frame per launch,
-    # serialized (AUTO: HYBRID for primary-only frames, FLAT for bounces; capi.cpp auto_sched)
+    # serialized (AUTO: HYBRID for primary-only frames, the path engine otherwise; capi.cpp auto_sched)
     roof_variant = variant
     if variant == E.ATR_KERNEL_AUTO:
-        roof_variant = E.ATR_KERNEL_HYBRID if bounces == 1 else E.ATR_KERNEL_FLAT
+        roof_variant = E.ATR_KERNEL_HYBRID if bounces == 1 and spp == 1 else E.ATR_KERNEL_PATHS
     s0 = streams[0]
 
     def time_one(v, n=10):
@@ -819,7 +817,7 @@ def run(args):
         # scene per launch) and the clustered scan's own-work bytes per ray at chip level (cache-level
         # traffic: above the HBM peak, which is why it cannot be the HBM fraction). VALU: the binding
         # resource, wave-instructions issued per second against the chip's issue peak.
-        clustered = args.variant in ("auto", "cl", "ps", "flat", "hyb")
+        clustered = args.variant in ("auto", "flat", "hyb", "paths")
         bpr = cluster_bytes_per_ray(live_ctr) if clustered else algorithmic_bytes_per_ray(live_ctr)
         step_s = elapsed / args.steps
         fpl = max(launch_frames)
@@ -842,7 +840,7 @@ def run(args):
             with open(os.path.join(ROOT, "tests", "golden", "goldens.json")) as f:
                 ctr = json.load(f)["hits"][gname]["counters"]
             roof["own_work"]["ref_bytes_per_ray"] = round(algorithmic_bytes_per_ray(ctr), 1)
-        kname = "persist_kernel" if args.variant == "ps" else "render_kernel"
+        kname = "path_" if roof_variant == E.ATR_KERNEL_PATHS else "render_kernel"
         roof["kernel"] = kname
         roof["variant"] = VARIANT_NAMES.get(roof_variant, roof_variant)
         # default: the compulsory model (no counters); replaced by the PMC-measured bytes below

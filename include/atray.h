@@ -49,8 +49,7 @@ typedef struct atr_octree atr_octree;
 
 /* load_model_data (OBJ_loader.h:6): custom parse_f64 (parser.h:113-191), faces keep the first
    triangle of each polygon, negative indices relative to the end. atr_mesh_load_obj parses on
-   the host's threads (threads = min(hardware threads, 16), ATR_PARSE_THREADS overrides);
-   atr_mesh_parse_obj on one. */
+   the host's threads (threads = min(hardware threads, 16)); atr_mesh_parse_obj on one. */
 int atr_mesh_load_obj(const char* path, atr_mesh** out);
 int atr_mesh_parse_obj(const char* text, size_t len, atr_mesh** out);
 /* The reference's parallel load (OBJ_loader.cpp:298-340): the text split into `threads`
@@ -164,7 +163,8 @@ typedef struct {
                                the way in, 0..1024; default 0 */
     int32_t hybrid_a, hybrid_b; /* HYBRID: a leaf step is dealt over the lanes when the largest
                                cluster count exceeds a x rounds + b, -4096..4096; default 2, 0 */
-    int32_t persist_chunk;  /* PERSIST: 8x8 cells per work-queue claim, 1..4096; default 16 */
+    int32_t path_batch_log2; /* PATHS: paths per batch = 2^this (the path queues hold one batch),
+                               12..30; default 27 (1920x1080 at 64 spp: one batch per frame) */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
     int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
                                dispatches its tiles' cells by that launch's measured cost, heaviest
@@ -172,7 +172,9 @@ typedef struct {
                                such launch); 0: list order; default 1. With an
                                atr_set_cell_plan plan for the image size it re-orders that plan's
                                block list */
-    int32_t reserved[5];    /* must be 0 */
+    int32_t path_camera_occ; /* PATHS: waves/SIMD of the camera-ray and bounce launches, 5..7, */
+    int32_t path_bounce_occ; /* or 0 = the measured default */
+    int32_t reserved[3];    /* must be 0 */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
 int atr_set_tuning(atr_ctx* ctx, const atr_tuning* tuning);
@@ -206,18 +208,23 @@ typedef struct {
     unsigned long long* traced_rays;
 } atr_frame;
 
-/* Kernel variant: AUTO picks the fastest exact variant. All variants are bit-identical. */
-enum { ATR_KERNEL_AUTO = 0, ATR_KERNEL_LANE = 1, ATR_KERNEL_WAVE = 2, ATR_KERNEL_TILE = 3,
-       ATR_KERNEL_TILE8 = 4, ATR_KERNEL_WAVEFRONT = 5, ATR_KERNEL_CLUSTER = 6,
-       ATR_KERNEL_PERSIST = 7 /* persistent waves, lanes refilled from per-XCD work queues */,
-       ATR_KERNEL_FLAT = 8 /* clustered scan, the wavefront's (ray, cluster) work dealt over its
-                              lanes in rounds (no control-flow divergence in the scan) */,
-       ATR_KERNEL_HYBRID = 9 /* per leaf step: lane-private scans when the rays' cluster counts
-                                are alike, FLAT rounds when one ray's leaf dominates */ };
+/* Kernel variant: AUTO picks the fastest exact variant (HYBRID for primary-only renders -- one
+   sample, bounce_limit 1, no AA -- else PATHS, or FLAT beyond 64 bounces). All variants are
+   bit-identical; any other value is ATR_E_INVALID. (Codes 2-7 were round-1..3 schedules measured
+   slower and removed) */
+enum { ATR_KERNEL_AUTO = 0,
+       ATR_KERNEL_LANE = 1 /* the reference's exact work: every triangle of every scanned leaf */,
+       ATR_KERNEL_FLAT = 8 /* cell megakernel: clustered scan, the wavefront's (ray, cluster) work
+                              dealt over its lanes in rounds, a pixel's samples in sequence */,
+       ATR_KERNEL_HYBRID = 9 /* cell kernel, per leaf step: lane-private scans when the rays' cluster
+                                counts are alike, FLAT rounds when one ray's leaf dominates */,
+       ATR_KERNEL_PATHS = 10 /* sample-parallel path engine: one lane per (pixel, sample) path, one
+                                launch per bounce over a queue of the live paths (<= 64 bounces) */ };
 
 /* start_render_from_camera: renders the pixels of `tiles` (inclusive rects; overlapping pixels
-   are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the null stream, HIP's convention). RNG: deterministic per-pixel PCG stream from `seed` (DESIGN.md "RNG"). Returns
-   immediately. */
+   are traced once) into `frame`, enqueued on `stream` (hipStream_t; NULL = the null stream, HIP's
+   convention). RNG: one deterministic PCG stream per (pixel, sample) from `seed`.
+   Returns immediately. */
 int atr_render_start(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                      const atr_frame* frame, uint64_t seed, void* stream);
 /* Progressive start for a live view (app.cpp:162-186): the tiles are rendered in list order,
@@ -233,8 +240,8 @@ int atr_render_start_ex(atr_ctx* ctx, const atr_camera* cam, const atr_tile* til
 /* Frames in flight in one launch (throughput, e.g. a live view rendering ahead): nframes renders
    of the same camera and tiles; frame f's outputs start frame_stride elements after frame f-1's
    (rgb: 3 x frame_stride floats; frame_stride >= the layout's pixels per frame). The cell
-   schedules run all frames as one grid, so one frame's slow cells overlap the next frame's;
-   PERSIST (multi-bounce AUTO) launches once per frame. Every frame equals atr_render_start_ex's
+   schedules run all frames as one grid, so one frame's slow cells overlap the next frame's; the
+   path engine runs the frames' cells as one list. Every frame equals atr_render_start_ex's
    output. */
 int atr_render_start_frames(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                             const atr_frame* frame, int32_t nframes, int64_t frame_stride, uint64_t seed,
@@ -259,30 +266,6 @@ int atr_render_tile_costs(atr_ctx* ctx, const atr_camera* cam, const atr_tile* t
    boxes tested and [9] primitives screened by the clustered scan. */
 int atr_render_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
                         uint64_t seed, int32_t variant, int64_t counters_out[10]);
-/* Diagnostic: one instrumented render; out = wave clocks (s_memtime, summed over waves) spent in
-   the FLAT/HYBRID scans' DFS passes, lane-private leaf scans, dealt leaf rounds, in the whole
-   wave, in each leaf step's preparation (leaf range, prefix sums, schedule decision), and in the
-   whole scan (tree query). The per-phase clocks are compiled only into a diagnostic build
-   (make EXTRA=-DATR_PHASE_CLOCKS); the product library reports the whole-wave clocks alone. */
-int atr_render_phase_clocks(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                            uint64_t seed, int32_t variant, int64_t out[6]);
-/* Diagnostic: one instrumented render; lane use of the bounce loop (cast_ray, renderer.cpp:213-262)
-   in the wavefront schedules (WAVE, FLAT, HYBRID): out[0..2] = wave steps of bounce 0, 1 and >= 2
-   (a step = one loop iteration some lane of the wave traces in), out[3..5] = lanes tracing in
-   them. out[3 + k] / (64 out[k]) is the lane utilisation of bounce bucket k. */
-int atr_render_path_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                             uint64_t seed, int32_t variant, int64_t out[6]);
-/* Diagnostic: one instrumented render; SIMD efficiency of the clustered scans: out[0] wave-level
-   iterations of the full-test candidate loops (two tests each in the paired loops), out[1] full
-   triangle tests, out[2] / out[3] DFS loop iterations at wave / lane level, out[4] dealt rounds,
-   out[5] the (ray, cluster) items they carried, out[6] traced rays. */
-int atr_render_simd_counters(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                             uint64_t seed, int32_t variant, int64_t out[7]);
-/* Diagnostic: one render of `tiles` recording, per 8x8 work block (block order), the wave's start
-   and end on the 100 MHz device clock and its HW_ID | XCC_ID << 32. out = 3 u64 per block;
-   with out == NULL (or cap too small) only *nblocks is set. */
-int atr_render_wave_trace(atr_ctx* ctx, const atr_camera* cam, const atr_tile* tiles, int32_t ntiles,
-                          uint64_t seed, int32_t variant, uint64_t* out, int64_t cap, int64_t* nblocks);
 /* Number of pixels a PACKED render of these tiles writes. */
 int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles);
 /* Host-only: pixel index (y * width + x) of every slot of a PACKED render of these tiles, in

@@ -595,16 +595,18 @@ static inline float rand_bi(uint64_t* st, uint64_t stream) {
     float rd = (float)om_pcg_u32(st, stream) * OM_INV_UINT32_MAX;
     return -1.0f + 2.0f * rd;
 }
-/* Deterministic per-pixel stream (documented deviation from renderer.cpp:376-378, whose
-   rdtsc*thread_id seeding makes the reference's multi-bounce RGB non-deterministic). */
+/* Deterministic stream per (pixel, sample) (documented deviation from renderer.cpp:376-378, whose
+   rdtsc*thread_id seeding makes the reference's multi-bounce RGB non-deterministic): state =
+   splitmix64(seed ^ pixel ^ sample << 40), increment 2 pixel + 1. Sample 0's stream is the
+   per-pixel stream of rounds 1-3. */
 static inline uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ULL;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
     return x ^ (x >> 31);
 }
-void om_pixel_rng(uint64_t seed, int64_t pixel_index, uint64_t* state, uint64_t* stream) {
-    *state = splitmix64(seed ^ (uint64_t)pixel_index);
+void om_path_rng(uint64_t seed, int64_t pixel_index, uint32_t sample, uint64_t* state, uint64_t* stream) {
+    *state = splitmix64(seed ^ (uint64_t)pixel_index ^ ((uint64_t)sample << 40));
     *stream = ((uint64_t)pixel_index << 1) | 1ULL;
 }
 
@@ -705,11 +707,12 @@ static void render_pixel(const om_scene* s, const om_camera* cm, uint64_t seed, 
                          om_counters* ctr, ov3* rgb, uint32_t* bgrx, uint32_t* casts) {
     float fy = film_y(cm, y), fx = film_x(cm, x);
     uint64_t st, stream;
-    om_pixel_rng(seed, (int64_t)y * cm->width + x, &st, &stream);
+    const int64_t pix = (int64_t)y * cm->width + x;
     ov3 col = v3(0, 0, 0);
     uint32_t c = 0;
     if (cm->anti_aliasing) { /* :336-347 */
         for (uint32_t i = 0; i < cm->spp; i++) {
+            om_path_rng(seed, pix, i, &st, &stream); /* one stream per (pixel, sample) */
             float xo = rand_bi(&st, stream) * cm->half_pixel_width + fx;
             float yo = rand_bi(&st, stream) * cm->half_pixel_height + fy;
             ov3 d = primary_dir(cm, xo, yo);
@@ -717,8 +720,10 @@ static void render_pixel(const om_scene* s, const om_camera* cm, uint64_t seed, 
         }
     } else { /* :348-357 */
         ov3 d = primary_dir(cm, fx, fy);
-        for (uint32_t i = 0; i < cm->spp; i++)
+        for (uint32_t i = 0; i < cm->spp; i++) {
+            om_path_rng(seed, pix, i, &st, &stream);
             col = vadd(col, cast_ray(s, cm->eye, d, cm->bounce_limit, &st, stream, &c, w, ctr));
+        }
     }
     col = vdiv(col, (float)cm->spp); /* :358 */
     *rgb = col;

@@ -130,7 +130,7 @@ double om_render_rows_threaded(const om_scene* s, const om_camera* cm, uint64_t 
 int32_t om_make_tiles(int32_t width, int32_t height, int32_t threads, int32_t* tiles_out, int32_t cap);
 
 uint32_t om_pcg_u32(uint64_t* state, uint64_t stream);
-void om_pixel_rng(uint64_t seed, int64_t pixel_index, uint64_t* state, uint64_t* stream);
+void om_path_rng(uint64_t seed, int64_t pixel_index, uint32_t sample, uint64_t* state, uint64_t* stream);
 
 #ifdef __cplusplus
 }

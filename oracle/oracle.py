@@ -131,7 +131,7 @@ def lib():
         L.om_make_tiles.restype = C.c_int32
         L.om_pcg_u32.argtypes = [P(C.c_uint64), C.c_uint64]
         L.om_pcg_u32.restype = C.c_uint32
-        L.om_pixel_rng.argtypes = [C.c_uint64, C.c_int64, P(C.c_uint64), P(C.c_uint64)]
+        L.om_path_rng.argtypes = [C.c_uint64, C.c_int64, C.c_uint32, P(C.c_uint64), P(C.c_uint64)]
         _lib = L
     return _lib
 

@@ -1,4 +1,4 @@
-"""GPU parity of the clustered leaf scan (ATR_KERNEL_CLUSTER) on inputs built to
+"""GPU parity of the clustered leaf scan (HYBRID, FLAT, PATHS) on inputs built to
 break it: near-grazing triangles whose det sits just above the culling tolerance (where the
 rounding bound of the cluster test is widest), back-facing copies, and exact duplicates of
 triangles (equal t, so the reference's leaf-order tie rule decides). Every pixel's face index
@@ -73,7 +73,7 @@ def test_cluster_scan_bit_exact_on_grazing_soup(eng, seed, n, det, leaf):
     eng.upload([SKY, MODEL], [(m, tree, m.aabb(), 1)], (), ())
     hit = face_o != 0xFFFFFFFF
     assert hit.sum() > 1000, hit.sum()   # the soup must actually be hit
-    variants = (E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID)
+    variants = E.VARIANTS
     if os.environ.get("ATR_TEST_VARIANTS"):
         variants = tuple(int(v) for v in os.environ["ATR_TEST_VARIANTS"].split(","))
     for variant in variants:

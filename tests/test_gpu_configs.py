@@ -5,9 +5,9 @@ The GPU renders the whole frame; the oracle (the reference algorithm restated, o
 re-renders row bands through the dragon's widest rows and its silhouette (grazing rays), and the
 band must match bit for bit: framebuffer, per-pixel ray_casts (renderer.cpp:260), primary hit
 face and t; RGB within 1e-5 relative (north star; in practice bit-exact). At full size the
-schedules must agree with each other (LANE: the reference's exact per-triangle work; FLAT: the
-multi-bounce default; CLUSTER: the primary-ray default; PERSIST: persistent lanes), a
-size-independent property.
+schedules must agree with each other (LANE: the reference's exact per-triangle work; PATHS: the
+sample-parallel multi-bounce default; FLAT and HYBRID: the cell megakernels), a size-independent
+property.
 Needs an MI355X (-m gpu)."""
 import os
 
@@ -101,10 +101,9 @@ C4_BANDS = [(552, 560), (312, 316)]
 C5_BANDS = [(1112, 1114), (626, 627)]
 
 
-@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
-                                     E.ATR_KERNEL_HYBRID] + EXTRA)
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID] + EXTRA)
 def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
-    """C4 through AUTO (= FLAT for multi-bounce, capi.cpp auto_sched), CLUSTER, PERSIST and HYBRID."""
+    """C4 through AUTO (= PATHS for multi-bounce, capi.cpp auto_sched), FLAT and HYBRID."""
     o = render(eng, E.camera(1920, 1080, 64, 5), variant)
     hitpx = sum(check_band(o, oracle_scene, O.Camera(1920, 1080, spp=64, bounces=5), a, b) for a, b in C4_BANDS)
     assert hitpx > 2000  # the bands cross the dragon
@@ -113,11 +112,11 @@ def test_c4_full_frame_band_matches_oracle(eng, oracle_scene, variant):
 
 def test_c4_schedules_agree_at_full_size(eng):
     """Size-independent property at C4: the reference's exact work (LANE), the multi-bounce
-    default (FLAT), the cell kernel (CLUSTER) and the persistent lanes (PERSIST) produce identical
-    frames, and a re-render is identical (determinism)."""
+    default (PATHS) and the cell megakernels (FLAT, HYBRID) produce identical frames, and a
+    re-render is identical (determinism: the path queues' order varies, the outputs do not)."""
     cam = E.camera(1920, 1080, 64, 5)
-    a = render(eng, cam, E.ATR_KERNEL_PERSIST)
-    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID):
+    a = render(eng, cam, E.ATR_KERNEL_PATHS)
+    for v in (E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID, E.ATR_KERNEL_PATHS):
         b = render(eng, cam, v)
         for k in ("fb", "casts", "face"):
             assert torch.equal(a[k], b[k]), (v, k)
@@ -137,8 +136,7 @@ def test_c5_full_frame_band_matches_oracle(eng, oracle_scene):
 ORBIT = [(0.1 + 0.5 * np.sin(a), 2.0, 0.5 * (1 - np.cos(a))) for a in np.linspace(0, 2 * np.pi, 7)[:-1]]
 
 
-@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST,
-                                     E.ATR_KERNEL_LANE, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID] + EXTRA)
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO] + list(E.VARIANTS) + EXTRA)
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (2, 3)])
 @pytest.mark.parametrize("layout", [E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED])
 def test_per_frame_cameras_equal_single_renders(eng, variant, spp, bounces, layout):

@@ -16,13 +16,11 @@ from tests.goldens import GOLD, SEED, hits, render  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 SKY, MODEL = O.SKY, O.MODEL_MAT
-# The parity triad: CLUSTER (primary-only default), PERSIST (multi-bounce default) and LANE (the
-# reference's exact per-triangle work). The slower experimental schedules (WAVE, TILE4/8,
-# WAVEFRONT) run only with ATR_TEST_ALL_VARIANTS=1.
-VARIANTS = [E.ATR_KERNEL_LANE, E.ATR_KERNEL_CLUSTER, E.ATR_KERNEL_PERSIST, E.ATR_KERNEL_FLAT, E.ATR_KERNEL_HYBRID]
-if os.environ.get("ATR_TEST_ALL_VARIANTS") == "1":
-    VARIANTS += [E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8, E.ATR_KERNEL_WAVEFRONT]
-# ATR_TEST_VARIANTS=a,b,...: exactly these kernel codes (experiment builds and diagnostic schedules)
+# Every variant of the shipping library: LANE (the reference's exact per-triangle work), the cell
+# kernels HYBRID (primary-only default) and FLAT (multi-bounce megakernel), and the sample-parallel
+# path engine PATHS (multi-bounce default).
+VARIANTS = list(E.VARIANTS)
+# ATR_TEST_VARIANTS=a,b,...: exactly these kernel codes (experiment builds)
 if os.environ.get("ATR_TEST_VARIANTS"):
     VARIANTS = [int(v) for v in os.environ["ATR_TEST_VARIANTS"].split(",")]
 RGB_RTOL = 1e-5
@@ -248,13 +246,13 @@ def test_cell_plan_changes_no_output(eng, variant):
 
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_tuning_changes_no_output(eng, variant):
-    """atr_set_tuning: XCD chunking, the HYBRID deal rule forced to always / never deal, the
-    PERSIST queue chunk and the cluster size (re-upload) change scheduling only -- every output
-    identical, primary and multi-bounce."""
+    """atr_set_tuning: XCD chunking, the HYBRID deal rule forced to always / never deal, the path
+    engine's batch size (2^12 paths: dozens of batches per frame) and the cluster size (re-upload)
+    change scheduling only -- every output identical, primary and multi-bounce."""
     W, H = 480, 270
     base = eng.tuning()
     settings = [{"xcd_chunk": 0}, {"xcd_chunk": 3}, {"hybrid_a": -4096, "hybrid_b": -4096},
-                {"hybrid_a": 4096, "hybrid_b": 4096}, {"persist_chunk": 1}, {"cluster_size": 7},
+                {"hybrid_a": 4096, "hybrid_b": 4096}, {"path_batch_log2": 12}, {"cluster_size": 7},
                 {"frame_plan": 0}]
     try:
         for spp, bounces in ((1, 1), (2, 3)):
@@ -345,12 +343,6 @@ def test_frames_per_launch_equal_single_renders(eng, variant, bounces):
     W, H = 96, 56
     cam = E.camera(W, H, 2, bounces)
     tiles = E.make_tiles(W, H, 4)
-    if variant == E.ATR_KERNEL_WAVEFRONT:
-        with pytest.raises(E.AtrError):
-            fb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-            eng.render_start_frames(cam, tiles, E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None,
-                                                             None, None), 2, W * H, SEED, variant=variant)
-        return
     for layout in (E.ATR_LAYOUT_IMAGE, E.ATR_LAYOUT_PACKED):
         want = run(eng, cam, tiles=tiles, layout=layout, variant=variant)
         n = W * H if layout == E.ATR_LAYOUT_IMAGE else E.packed_size(tiles)
@@ -413,10 +405,6 @@ def test_progressive_start_equals_one_shot(eng, variant):
     tiles = E.make_tiles(W, H, 8)
     cam = E.camera(W, H, 3, 4)
     want = run(eng, cam, tiles=tiles, variant=variant)
-    if variant == E.ATR_KERNEL_WAVEFRONT:
-        with pytest.raises(E.AtrError):
-            run(eng, cam, tiles=tiles, variant=variant, progressive=7)
-        return
     for per in (1, 7, 1000):
         got = run(eng, cam, tiles=tiles, variant=variant, progressive=per)
         for k in ("fb", "casts", "face", "rgb", "traced"):
@@ -478,13 +466,15 @@ def test_spheres_and_planes_match_oracle(eng, variant):
 
 
 def test_variants_agree_at_full_size_multibounce(eng):
-    """Size-independent properties at the config-4 resolution (1920x1080, 4 spp, 5 bounces):
-    both traversal schedules agree bit for bit, and a re-render is identical (determinism)."""
+    """Size-independent properties at the config-4 resolution (1920x1080, 4 spp, 5 bounces): the
+    reference-work cell kernel (LANE) and the sample-parallel path engine agree bit for bit, and a
+    re-render is identical (determinism: the path queues' order varies between runs, the outputs
+    do not)."""
     upload(eng, "Dragon", True)
     cam = E.camera(1920, 1080, 4, 5)
     a = run(eng, cam, variant=E.ATR_KERNEL_LANE)
-    b = run(eng, cam, variant=E.ATR_KERNEL_WAVE)
-    c = run(eng, cam, variant=E.ATR_KERNEL_WAVE)
+    b = run(eng, cam, variant=E.ATR_KERNEL_PATHS)
+    c = run(eng, cam, variant=E.ATR_KERNEL_PATHS)
     for k in ["fb", "casts", "face"]:
         assert np.array_equal(a[k], b[k]) and np.array_equal(b[k], c[k])
     assert np.array_equal(a["rgb"].view(np.uint32), b["rgb"].view(np.uint32))
@@ -503,7 +493,7 @@ def test_gpu_work_counters_equal_reference_work(eng, name, variant):
     c = eng.counters(E.camera(g["W"], g["H"]), [[0, 0, g["W"] - 1, g["H"] - 1]], SEED, variant)
     for k in ["n_rays", "n_box", "n_leaf"]:
         assert c[k] == g["counters"][k], (k, c[k], g["counters"][k])
-    exact_work = (E.ATR_KERNEL_LANE, E.ATR_KERNEL_WAVE, E.ATR_KERNEL_TILE, E.ATR_KERNEL_TILE8, E.ATR_KERNEL_WAVEFRONT)
+    exact_work = (E.ATR_KERNEL_LANE,)
     if variant not in exact_work and g["tree"]:
         # the clustered scan visits the same leaves but skips provably irrelevant triangles
         assert 0 < c["n_tri"] <= g["counters"]["n_tri"], (c["n_tri"], g["counters"]["n_tri"])

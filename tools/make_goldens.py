@@ -8,7 +8,7 @@ brute-force hit/difference counts. This script re-checks those pins and then wri
   goldens.json          hashes, hit counts, tree stats, per-ray work counters per config
   hits_<name>.npz       per-pixel primary hit (face u32, t f32 bits), lzma-packed
   render_<name>.npz     multi-bounce RGB (f32, pre-clamp) + BGRX + per-pixel ray_casts
-                        under the deterministic per-pixel PCG stream (DESIGN.md "RNG")
+                        under the deterministic PCG stream per (pixel, sample)
 
 usage: python tools/make_goldens.py
 """
@@ -43,6 +43,10 @@ RENDER_CONFIGS = [
     ("deer_256x144_s2_b5", "Deer", 256, 144, True, 2, 5, False),
     ("dragon_240x135_s2_b5", "Dragon", 240, 135, True, 2, 5, False),
     ("monkey_160x90_s2_b2_bf", "Monkey", 160, 90, False, 2, 2, False),
+    # round 4: the path engine's shapes -- one pixel per wavefront (64 spp, ragged cells), and a
+    # pixel's samples straddling wavefronts (100 spp) with AA jitter
+    ("dragon_120x68_s64_b5", "Dragon", 120, 68, True, 64, 5, False),
+    ("monkey_72x40_s100_b3_aa", "Monkey", 72, 40, True, 100, 3, True),
 ]
 
 
