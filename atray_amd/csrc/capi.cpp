@@ -451,8 +451,12 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
     if ((rc = ensure_buf(bs->cost_last, size_t(nb) * sizeof(unsigned long long), false))) return rc;
     if ((rc = ensure_buf(bs->plan_work, atr_plan_work_bytes(nb), true))) return rc;
     if ((rc = ensure_buf(bs->plan_blocks, size_t(nb + max_split) * sizeof(DBlock), false))) return rc;
-    if (!bs->plan_ready && !fresh)  // a rebuilt set reuses buffers a plan may not have cleared
+    if (!bs->plan_ready && !fresh) {  // a rebuilt set reuses buffers a plan may not have cleared
         HIPCHK(hipMemsetAsync(bs->cost.p, 0, size_t(nb) * sizeof(unsigned long long), s));
+        // and the work area's thresholds (learned on the old list, whose nb and max_split differ):
+        // back to the documented zeroed state (class 0, no split) for the first plan on this list
+        HIPCHK(hipMemsetAsync(bs->plan_work.p, 0, atr_plan_work_bytes(nb), s));
+    }
     bs->max_split = max_split;
     if (bs->plan_ready) {
         P.blocks = static_cast<const DBlock*>(bs->plan_blocks.p);

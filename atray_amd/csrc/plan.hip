@@ -66,7 +66,7 @@ __device__ __forceinline__ int block_class(const Thresholds& T, int bkt) {
     return k;
 }
 
-// a zeroed Thresholds (the first plan) gives class 0 and 4 waves to every cell: split thresholds
+// a zeroed Thresholds (the first plan) gives class 0 and one wave to every cell: split thresholds
 // of 0 are replaced by "no split" (kPlanBuckets) when derived, so 0 only occurs before the first
 __device__ __forceinline__ int block_parts(const Thresholds& T, int bkt) {
     if (T.split_thr == 0) return 1;

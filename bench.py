@@ -107,27 +107,35 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2.0  # wave-instructions/s: 1,024 SIMD-32s, 
                                           # (MI355X_MICROARCH.md "Wave scheduling"), 2.4 GHz
 
 
-def pmc_counters(args, kernel_name):
+def pmc_counters(args, kernel_name, path_tail=None):
     """Counters of the timed launches of THIS command's shape: a child run of bench.py with the same
-    --config/--steps/--warmup/--streams/--frames-per-launch/--variant (no PMC, no CPU baseline),
-    profiled by separate rocprofv3 --pmc passes. Per counter: the mean over the launches of the
-    largest render grid (the timed launches; warmup and priming launches are smaller or equal in
-    shape and are excluded when smaller). Returns ({counter: mean per launch}, frames per such
-    launch, note)."""
+    --config/--steps/--warmup/--streams/--frames-per-launch/--variant/--tuning (--pmc-child: no PMC,
+    no CPU baseline, and nothing rendered after the timed region), profiled by separate rocprofv3
+    --pmc passes (--kernel-trace only).
+      cell kernels (kernel_name "render_kernel"): the dispatches of the largest render grid (the
+        timed launches; warmup and priming launches are smaller) -- per counter the mean per launch;
+      path engine (path_tail = {kernel: n}): the last n dispatches of each path kernel (the timed
+        region is the child's last work) -- per counter the sum over them.
+    The selected rows are written to gpurun_out/bench_pmc/rows_<config>.json (kernel, grid,
+    dispatch, counter, value) so the line can be recomputed from them (tools/collect_r04.py copies
+    them into profiles/). Returns ({counter: value}, {"grid" | "dispatches": ...}, note)."""
     exe = "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
-        return None, 0, "rocprofv3 missing"
+        return None, None, "rocprofv3 missing"
     out = {}
-    grid = None
+    info = {}
+    kept = []
     base = os.path.join(ROOT, "gpurun_out", "bench_pmc")
     for i, group in enumerate(PMC_PASSES):
-        d = os.path.join(base, f"pass{i}")
+        d = os.path.join(base, f"{args.config}_pass{i}")
         os.makedirs(d, exist_ok=True)
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            os.remove(f)  # a previous run's rows never mix into this one
         cmd = [exe, "--pmc", *group, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup",
                str(args.warmup), "--frames-per-launch", str(args.frames_per_launch), "--streams", str(args.streams),
                "--config", args.config, "--variant", args.variant, "--no-cpu-baseline", "--no-pmc", "--no-prep",
-               "--no-steady"]
+               "--no-steady", "--pmc-child"] + (["--tuning", args.tuning] if args.tuning else [])
         env = dict(os.environ)
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
             env.pop(k, None)
@@ -135,25 +143,61 @@ def pmc_counters(args, kernel_name):
             subprocess.run(cmd, check=True, timeout=300, env=env, stdout=subprocess.DEVNULL,
                            stderr=subprocess.DEVNULL)
         except Exception as e:  # noqa: BLE001
-            return None, 0, f"rocprofv3 {group} failed: {e}"
+            return None, None, f"rocprofv3 {group} failed: {e}"
         rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
-                    # product launches only (not the instrumented COUNT build: <.., true, ..>)
-                    if kernel_name in name and not re.search(kernel_name + r"<(\d+, )?true", name):
-                        rows.append((int(row.get("Grid_Size") or 0), row.get("Dispatch_Id"), row["Counter_Name"],
-                                     float(row["Counter_Value"])))
+                    # product launches only (not the instrumented COUNT builds: <.., true, ..>)
+                    if kernel_name in name and not re.search(r"<(\d+, )?true", name):
+                        rows.append((name, int(row.get("Grid_Size") or 0), int(row.get("Dispatch_Id") or 0),
+                                     row["Counter_Name"], float(row["Counter_Value"])))
         if not rows:
-            return None, 0, f"no rows for {group}"
-        big = max(g for g, _, _, _ in rows)
-        grid = big if grid is None else grid
-        for c in group:
-            vals = [v for g, _, n, v in rows if g == big and n == c]
-            if vals:
-                out[c] = sum(vals) / len(vals)
-    return out, grid, "ok"
+            return None, None, f"no rows for {group}"
+        if path_tail is None:
+            big = max(r[1] for r in rows)
+            info["grid"] = big
+            sel = [r for r in rows if r[1] == big]
+            for c in group:
+                vals = [r[4] for r in sel if r[3] == c]
+                if vals:
+                    out[c] = sum(vals) / len(vals)
+        else:
+            sel = []
+            for kn, n in path_tail.items():
+                ids = sorted({r[2] for r in rows if kn in r[0]})[-n:] if n else []
+                if len(ids) < n:
+                    return None, None, f"{kn}: {len(ids)} dispatches, want {n}"
+                idset = set(ids)
+                sel += [r for r in rows if kn in r[0] and r[2] in idset]
+                info.setdefault("dispatches", {})[kn] = n
+            for c in group:
+                out[c] = sum(r[4] for r in sel if r[3] == c)
+                for kn in path_tail:
+                    info.setdefault("per_kernel", {}).setdefault(kn, {})[c] = sum(
+                        r[4] for r in sel if r[3] == c and kn in r[0])
+        kept += sel
+    with open(os.path.join(base, f"rows_{args.config}.json"), "w") as fh:
+        json.dump({"config": args.config, "steps": args.steps, "warmup": args.warmup, "tuning": args.tuning,
+                   "selection": "largest grid" if path_tail is None else {"last dispatches": path_tail},
+                   "columns": ["kernel", "grid", "dispatch", "counter", "value"], "rows": kept}, fh)
+    return out, info, "ok"
+
+
+def path_dispatches(args, tiles, W, H, spp, bounces, batch_log2):
+    """Kernel dispatches of the path engine in the timed region (capi.cpp launch_paths): per
+    launch of nf frames, its nf x blocks cells in batches of 2^batch_log2 / (64 spp) cells; per
+    batch one camera, bounces - 1 bounce and one resolve launch."""
+    cells = set()
+    for x0, y0, x1, y1 in tiles:
+        for cy in range(max(0, y0) // 8, min(H - 1, y1) // 8 + 1):
+            for cx in range(max(0, x0) // 8, min(W - 1, x1) // 8 + 1):
+                cells.add((cx, cy))
+    per_batch = max(1, (1 << batch_log2) // (64 * max(1, spp)))
+    nb = sum(-(-nf * len(cells) // per_batch) for nf in launch_sizes(args.steps, args.frames_per_launch,
+                                                                      max(1, args.streams)))
+    return {"path_camera_kernel": nb, "path_bounce_kernel": nb * max(0, bounces - 1), "path_resolve_kernel": nb}
 
 
 def cpu_baseline(asset, W, H, spp, bounces, use_tree, seconds):
@@ -283,14 +327,16 @@ def main():
                     help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
     ap.add_argument("--exchange", default="bgr", choices=["bgr", "bgrx"],
                     help="N>1 frame exchange: 3 bytes per pixel (the framebuffer's X byte is always 0; "
-                         "atr_pack_bgr / atr_scatter_bgr) or the u32 BGRX framebuffer (gloo rehearsals always "
-                         "use bgrx)")
+                         "atr_pack_bgr / atr_scatter_bgr; gloo rehearsals stage the bytes through the host) or the "
+                         "u32 BGRX framebuffer")
     ap.add_argument("--check", action="store_true",
                     help="rank 0: compare every assembled frame with a one-launch full-frame render")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostic, one process: render only rank --sim-rank's shard of a --sim-world plan "
                          "(packed outputs, per-tile ray_casts sums; no exchange): the per-rank render side of an N-GPU run")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--pmc-child", action="store_true",
+                    help="internal (the PMC passes' child run): stop right after the timed region")
     ap.add_argument("--selftest", action="store_true",
                     help="CPU only: synthetic fill instead of the render kernel (launch/plan/gather test)")
     args = ap.parse_args()
@@ -502,9 +548,10 @@ def run(args):
             cell_split["prio_frac"] = args.cell_prio
         eng.set_cell_plan(W, H, cplan)
     if pw > 1 or args.single_tiles == "cost":
-        tiles = E.tiles_array(plan.tiles[pr])
+        tiles_list = [list(t) for t in plan.tiles[pr]]
     else:
-        tiles = E.tiles_array([[0, 0, W - 1, H - 1]])
+        tiles_list = [[0, 0, W - 1, H - 1]]
+    tiles = E.tiles_array(tiles_list)
     S_, F_ = max(1, args.streams), args.frames_per_launch
     # --stream-priority: stream 0 at the device's highest priority, so its launch's workgroups are
     # dispatched first and it completes early; the other streams' work fills its tail, and at
@@ -517,7 +564,9 @@ def run(args):
     own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
     npx = W * H
     on_host = world > 1 and backend != "nccl"
-    bgr = pw > 1 and args.exchange == "bgr" and not on_host  # 3-byte exchange (device kernels)
+    # 3-byte exchange (atr_pack_bgr / atr_scatter_bgr on the device; a gloo rehearsal stages the
+    # packed bytes through the host)
+    bgr = pw > 1 and args.exchange == "bgr"
     traced = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
     # per stream slot: F framebuffers and F ray_casts images (u32), frames back to back
     casts = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
@@ -539,6 +588,8 @@ def run(args):
             fbs = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
             if rank == 0 and not sim:
                 big = [torch.zeros(3 * F_ * npx, dtype=torch.uint8, device=dev) for _ in range(S_)]
+                if on_host:  # gloo: the gather lands in host memory, then goes to the device
+                    bigh = [torch.zeros(3 * F_ * npx, dtype=torch.uint8) for _ in range(S_)]
                 dst_idx = torch.from_numpy(S.frames_assembly_index(plan, F_)).to(dev)
                 images = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
                 send3 = [b_[3 * off[0]:3 * off[0] + 3 * F_ * own] for b_ in big]
@@ -580,6 +631,8 @@ def run(args):
             for w_ in works:
                 w_.wait()
             if rank == 0 and bgr:
+                if on_host:
+                    big[q].copy_(bigh[q])
                 eng.scatter_bgr(big[q].data_ptr(), big[q].numel() // 3, dst_idx.data_ptr(), images[q].data_ptr(),
                                 stream=streams[q].cuda_stream)
             elif rank == 0:
@@ -619,7 +672,14 @@ def run(args):
                     pending[j] = (q, [])
                     return
                 if bgr:
-                    works = S.gather_frames(send3[q], big[q] if rank == 0 else None, plan, rank, nf, dist, unit=3)
+                    if on_host:
+                        torch.cuda.synchronize()
+                        send = send3[q][:3 * nf * own].cpu()
+                        if rank == 0:
+                            bigh[q][3 * off[0]:3 * off[0] + 3 * nf * own] = send
+                        works = S.gather_frames(send, bigh[q] if rank == 0 else None, plan, rank, nf, dist, unit=3)
+                    else:
+                        works = S.gather_frames(send3[q], big[q] if rank == 0 else None, plan, rank, nf, dist, unit=3)
                     works.append(dist.reduce(ts, dst=0, async_op=True))
                     pending[j] = (q, works)
                     return
@@ -673,6 +733,11 @@ def run(args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timing[0] = False
+    if args.pmc_child:  # the profiler's view: the timed region is this process's last GPU work
+        eng.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return
     launch_done = [round(ev0.elapsed_time(e), 3) for _, _, e in launch_ev]  # ms after the timed region's start
     launch_ms = [a.elapsed_time(e) for _, a, e in launch_ev]  # each timed launch's render, on its stream
     launch_frames = [nf for nf, _, _ in launch_ev]
@@ -848,8 +913,43 @@ def run(args):
         roof["frac"] = roof["compulsory"]["frac"]
         roof["traffic"] = None
         roof["source"] = "compulsory bytes (no PMC)"
-        if world == 1 and not args.no_pmc:
-            pmc, grid, why = pmc_counters(args, kname)
+        paths = roof_variant == E.ATR_KERNEL_PATHS
+        if world == 1 and not args.no_pmc and paths:
+            # the path engine: every kernel of the timed frames (camera, bounces, resolve), per frame
+            tail = path_dispatches(args, tiles_list, W, H, spp, bounces, eng.tuning()["path_batch_log2"])
+            pmc, info, why = pmc_counters(args, "path_", tail)
+            roof["pmc_note"] = why
+            roof["kernel"] = "path engine: path_camera_kernel + path_bounce_kernel x (bounces - 1) + path_resolve_kernel"
+            if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+                K = args.steps
+                per_frame = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0 / K
+                roof["traffic"] = round(per_frame)
+                roof["traffic_per_frame"] = round(per_frame)
+                roof["traffic_per_traced_ray"] = round(per_frame / (rays_total / K), 1)
+                roof["pmc_frames"] = {"frames": K, "dispatches": info["dispatches"],
+                                      "fetch_bytes_per_frame": round(2.0 * pmc["FETCH_SIZE"] * 1024.0 / K),
+                                      "write_bytes_per_frame": round(pmc["WRITE_SIZE"] * 1024.0 / K),
+                                      "per_kernel_bytes_per_frame": {
+                                          kn: round((2.0 * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0)) * 1024.0 / K)
+                                          for kn, v in info["per_kernel"].items()}}
+                roof["achieved"] = round(per_frame / step_s / 1e9, 2)
+                roof["frac"] = round(per_frame / step_s / 1e9 / HBM_PEAK_GBS, 5)
+                roof["source"] = "PMC bytes of the timed frames' path kernels / frames / measured time per frame"
+            if pmc and "SQ_INSTS_VALU" in pmc:
+                valu_frame = pmc["SQ_INSTS_VALU"] / args.steps
+                roof["valu"] = {"bound": "valu-issue", "wave_insts_per_frame": round(valu_frame),
+                                "achieved": round(valu_frame / step_s / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+                                "unit": "G wave-instr/s", "frac": round(valu_frame / step_s / VALU_ISSUE_PEAK, 4),
+                                "wait_frac": round(pmc.get("SQ_WAIT_ANY", 0.0) / max(1.0, pmc.get("SQ_WAVE_CYCLES", 1.0)), 4),
+                                "waves_per_frame": round(pmc.get("SQ_WAVES", 0.0) / args.steps),
+                                "per_kernel_insts_per_frame": {kn: round(v.get("SQ_INSTS_VALU", 0.0) / args.steps)
+                                                               for kn, v in info["per_kernel"].items()}}
+            if pmc and "TCC_HIT_sum" in pmc:
+                h, m = pmc["TCC_HIT_sum"], pmc.get("TCC_MISS_sum", 0.0)
+                roof["l2_hit_rate"] = round(h / max(1.0, h + m), 4)
+        elif world == 1 and not args.no_pmc:
+            pmc, info, why = pmc_counters(args, kname)
+            grid = info["grid"] if info else None
             roof["pmc_note"] = why
             if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
                 # FETCH_SIZE doubled (MI355X_MICROARCH.md, HBM: gfx950 reports half the bytes of wide

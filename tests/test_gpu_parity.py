@@ -244,6 +244,39 @@ def test_cell_plan_changes_no_output(eng, variant):
         eng.set_cell_plan(W, H, np.full(((W + 7) // 8) * ((H + 7) // 8), 0x45, np.uint8))
 
 
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_HYBRID, E.ATR_KERNEL_FLAT])
+def test_cell_plan_under_frame_plan_changes_no_output(eng, variant):
+    """A user cell plan with 2/4/8-way splits and classes, the single-frame plan on top of it
+    (frame_plan=1 re-plans the split list launch after launch, plan.hip): the same tiles rendered
+    three times equal the frame_plan=0 render, image and packed layouts."""
+    upload(eng, "Dragon", True)
+    W, H = 480, 270
+    rng = np.random.default_rng(11)
+    base = eng.tuning()
+    ncell = ((W + 7) // 8) * ((H + 7) // 8)
+    plan = rng.choice(np.array([0, 2, 4, 8], np.uint8), size=ncell, p=[0.7, 0.1, 0.1, 0.1])
+    plan |= rng.choice(np.array([0, E.plan_class(7), E.plan_class(2)], np.uint8), size=ncell, p=[0.6, 0.2, 0.2])
+    try:
+        for spp, bounces in ((1, 1), (2, 3)):
+            cam = E.camera(W, H, spp, bounces)
+            tiles = E.make_shard_tiles(W, H, 64, 0, 2)
+            eng.set_cell_plan(W, H, plan)
+            eng.set_tuning(frame_plan=0)
+            want = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
+                                                         variant=variant)]
+            eng.set_tuning(frame_plan=1)
+            for _ in range(3):  # the same block set each time: the planned list is dispatched
+                got = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
+                                                            variant=variant)]
+                for a, b in zip(want, got):
+                    for k in ("fb", "face", "t", "casts", "rgb"):
+                        assert np.array_equal(np.asarray(a[k]).view(np.uint32), np.asarray(b[k]).view(np.uint32)), k
+                    assert a["traced"] == b["traced"]
+    finally:
+        eng.set_cell_plan(W, H, None)
+        eng.set_tuning(**base)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_tuning_changes_no_output(eng, variant):
     """atr_set_tuning: XCD chunking, the HYBRID deal rule forced to always / never deal, the path
