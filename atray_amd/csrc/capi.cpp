@@ -513,9 +513,15 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     const int64_t batch = std::max<int64_t>(1, (int64_t(1) << c->tune.path_batch_log2) / per_cell);
     const int64_t cells = std::min<int64_t>(batch, P.nblocks);
     const int32_t levels = std::max(bl, 1);
+    // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
+    // one-frame launch already holds the batch of the multi-frame launches that follow it (a
+    // regrowth waits for every stream of the context)
+    int64_t cap = 1;
+    while (cap < cells * per_cell) cap <<= 1;
+    cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
     atr_ctx::PathWS* ws = nullptr;
     hipError_t e;
-    if ((e = path_workspace(c, s, cells * per_cell, levels, ws)) != hipSuccess) return e;
+    if ((e = path_workspace(c, s, cap, std::max(levels, 8), ws)) != hipSuccess) return e;
     PathParams Q;
     std::memset(&Q, 0, sizeof(Q));
     Q.cam = P.cam;

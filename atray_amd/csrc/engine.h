@@ -204,12 +204,14 @@ struct RenderParams {
 
 // Sample-parallel path engine (paths.hip): one lane per (pixel, sample) path. A batch
 // is a contiguous range [cell0, cell0 + ncells) of the launch's cell list (frames interleaved as in
-// RenderParams: cell c renders block c / nf of frame c % nf); its paths are numbered
-// g = (c - cell0) x 64 spp + pixel lane x spp + sample, so every wavefront of 64 consecutive paths
-// lies in one cell. Path records between bounces are four float4 planes of `cap` entries each:
+// RenderParams: cell c renders block c / nf of frame c % nf). The camera launch's wavefront w of
+// the batch takes paths r = 64 w .. 64 w + 63 of cell w / spp (r -> pixel lane r / spp, sample
+// r % spp: a pixel's samples side by side), so a wavefront lies in one cell. Path records between
+// bounces are four float4 planes of `cap` entries each:
 //   p0 = {o.xyz, d.x}, p1 = {d.y, d.z, bits(pixel), bits(g)}, p2 = {ret.xyz, w.x},
 //   p3 = {w.y, w.z, bits(rng lo), bits(rng hi)};
-// a finished path leaves {colour.xyz, bits(ray_casts)} in out[g].
+// a finished path leaves {colour.xyz, bits(ray_casts)} in its result slot
+// out[g], g = (c - cell0) x 64 spp + sample x 64 + pixel lane.
 constexpr int kPathPlanes = 4;
 // Per bounce level k of a batch (zeroed before the batch): the launch of level k (0 = the camera
 // rays) appends its surviving paths to queue k & 1 (tail); the bounce launch k + 1 reads them,

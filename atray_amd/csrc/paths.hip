@@ -41,9 +41,11 @@ __device__ __forceinline__ size_t out_index(int32_t layout, int32_t width, int64
     return o + size_t(fidx) * size_t(frame_stride);
 }
 
-// A finished path: its colour (cast_ray's ret) and the reference's ray_casts (renderer.cpp:260).
-__device__ __forceinline__ void path_finish(float4_t* out, int64_t g, V3 ret, uint32_t casts) {
-    out[g] = float4_t{ret.x, ret.y, ret.z, __uint_as_float(casts)};
+// A finished path: its colour (cast_ray's ret) and the reference's ray_casts (renderer.cpp:260),
+// at its result slot o (cell x 64 spp + sample x 64 + pixel lane: the resolve's lanes read a
+// sample's 64 results as one coalesced 1-KB row).
+__device__ __forceinline__ void path_finish(float4_t* out, uint32_t o, V3 ret, uint32_t casts) {
+    out[o] = float4_t{ret.x, ret.y, ret.z, __uint_as_float(casts)};
 }
 
 // Append this lane's path (if `go`) to queue q (planes `cap` entries apart): one atomic per wave for
@@ -76,6 +78,22 @@ __device__ __forceinline__ void path_counters(unsigned long long* C, const Ctr& 
         if (lane == 0 && t) atomicAdd(C + k, (unsigned long long)t);
     }
     if (lane == 0) atomicAdd(C + 7, 1ull);
+    // [10..15] wave clocks of the scan phases (DIAG build only; zero otherwise), [22..26] SIMD use
+    if (lane == 0) {
+        atomicAdd(C + 10, (unsigned long long)ct.t_pass);
+        atomicAdd(C + 11, (unsigned long long)ct.t_lp);
+        atomicAdd(C + 12, (unsigned long long)ct.t_deal);
+        atomicAdd(C + 14, (unsigned long long)ct.t_prep);
+        atomicAdd(C + 15, (unsigned long long)ct.t_scan);
+    }
+    uint32_t e[5] = {ct.cand_wave, ct.node_wave, ct.node_lane, ct.round_wave, ct.round_items};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        uint32_t x = e[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        if (lane == 0 && x) atomicAdd(C + 22 + k, (unsigned long long)x);
+    }
 }
 
 // ------------------------------------------------------------------ camera rays + first shading
@@ -90,7 +108,7 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
     const uint32_t r = uint32_t(wv - int64_t(cellrel) * spp) * 64u + uint32_t(lane);  // path within the cell
     const int pl = int(r / spp);  // the pixel's lane in the 8x8 cell
     const uint32_t s = r - uint32_t(pl) * spp;  // its sample
-    const int64_t g = int64_t(cellrel) * 64 * spp + r;
+    const uint32_t g = uint32_t(cellrel) * 64u * spp + s * 64u + uint32_t(pl);  // result slot
     int32_t fidx, bi;
     cell_of(P.frame_blocks, P.nblocks, P.cell0 + cellrel, fidx, bi);
     const DBlock blk = P.blocks[bi];
@@ -138,7 +156,7 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
             else go = true;
         }
     }
-    path_enqueue(P.q[0], P.cap, &P.ctl[0], go, o, d, uint32_t(pix), uint32_t(g), ret, w, st);
+    path_enqueue(P.q[0], P.cap, &P.ctl[0], go, o, d, uint32_t(pix), g, ret, w, st);
     const uint32_t traced = active ? 1u : 0u;
     if (P.traced_rays) add_traced(P.traced_rays, traced, int(wv));
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
@@ -227,13 +245,13 @@ __global__ __launch_bounds__(256) void path_resolve_kernel(PathParams P) {
     const atr_camera& cm = P.nfcam > 0 ? P.fcam[__builtin_amdgcn_readfirstlane(fidx)] : P.cam;
     const uint32_t spp = cm.samples_per_pixel;
     const bool traced = cm.bounce_limit > 0;
-    const float4_t* src = P.out + (int64_t(cellrel) * 64 + lane) * int64_t(spp);
+    const float4_t* src = P.out + int64_t(cellrel) * 64 * int64_t(spp) + lane;
     V3 col = mk(0.f, 0.f, 0.f);
     uint32_t casts = 0;
     for (uint32_t s = 0; s < spp; ++s) {  // col += cast_ray(...) in sample order (:353-356)
         V3 c = mk(0.f, 0.f, 0.f);
         if (traced) {
-            const float4_t v = src[s];
+            const float4_t v = src[64 * int64_t(s)];
             c = mk(v.x, v.y, v.z);
             casts += __float_as_uint(v.w);
         }

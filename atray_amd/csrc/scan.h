@@ -247,8 +247,11 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
 // (t, leaf rank)), so the choice changes no output bit. Without HYB every step deals (FLAT).
 // LDSB: the DFS pass inserts straight into the LDS columns instead of a register buffer copied after
 // it. UO: one origin for the whole wave (camera rays). UT: the wave walks its passes together
-// (traverse_pass_wave: coherent rays). NUV: u and v feed no output (primary-only frames).
-template <bool COUNT, bool HYB = false, bool LDSB = false, bool UO = false, bool UT = false, bool NUV = false>
+// (traverse_pass_wave: coherent rays). NUV: u and v feed no output (primary-only frames). NEAR (with
+// LDSB, per-lane passes): near-first passes that skip subtrees beyond the full buffer
+// (traverse_pass_near: incoherent bounce rays).
+template <bool COUNT, bool HYB = false, bool LDSB = false, bool UO = false, bool UT = false, bool NUV = false,
+          bool NEAR = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     constexpr int K = kLeafBuf;
@@ -305,7 +308,8 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 LdsLeafBuf<K> lb;
                 lb.d = &s_lbd[w][0][ln];
                 lb.leaf = &s_lbl[w][0][ln];
-                n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+                if constexpr (NEAR) n = traverse_pass_near<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+                else n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
             } else {  // register buffer: the LDS one measured 5% slower for incoherent bounce rays
                 LeafBuf<K> lb;
                 n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
@@ -473,8 +477,8 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                 tree_closest_flat<COUNT, true, true, true, true, true>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else if constexpr (FLAV == FLAV_HYB_BOUNCE)
                 tree_closest_flat<COUNT, true, false, false, false, false>(r, m, active, h, err, ct, hyb_a, hyb_b);
-            else  // bounce rays: LDS leaf buffer, every step dealt
-                tree_closest_flat<COUNT, false, true, false, false, false>(r, m, active, h, err, ct);
+            else  // bounce rays: near-first passes into the LDS leaf buffer, every step dealt
+                tree_closest_flat<COUNT, false, true, false, false, false, true>(r, m, active, h, err, ct);
             if (h.t > kTol && h.t < best) { best = h.t; face = h.face; fu = h.u; fv = h.v; nm = i; }
         } else if (active) {  // brute force (:58-82), face-ordered triangles, uniform loads
             if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }

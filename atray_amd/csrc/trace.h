@@ -228,12 +228,38 @@ struct LdsLeafBuf {
     int32_t* leaf;  // column base of the leaf ids
     int32_t n;      // entries held
     float thr;      // d[K - 1] when full, else +inf: an insert needs dis < thr
+    int32_t thr_leaf;  // leaf[K - 1] when full (near-first passes: (dis, rank) order)
 };
 
 template <int K>
 __device__ __forceinline__ void lb_clear(LdsLeafBuf<K>& b) {
     b.n = 0;
     b.thr = __builtin_inff();
+    b.thr_leaf = 0x7FFFFFFF;
+}
+
+// Insert in (distance, rank) order for passes that discover leaves out of rank order
+// (traverse_pass_near): a leaf goes behind every entry that precedes it in that order -- the
+// position the stable insertion sort (kd_tree.cpp:392-410) gives it, since its discovery order IS
+// the rank order.
+template <int K>
+__device__ __forceinline__ void lb_insert_lex(LdsLeafBuf<K>& b, float dis, int32_t leaf) {
+    if (!(dis < b.thr || (dis == b.thr && leaf < b.thr_leaf))) return;
+    int j = b.n < K ? b.n : K - 1;
+    for (; j > 0; --j) {
+        const float pd = b.d[64 * (j - 1)];
+        const int32_t pl = b.leaf[64 * (j - 1)];
+        if (!(pd > dis || (pd == dis && pl > leaf))) break;
+        b.d[64 * j] = pd;
+        b.leaf[64 * j] = pl;
+    }
+    b.d[64 * j] = dis;
+    b.leaf[64 * j] = leaf;
+    if (b.n < K) ++b.n;
+    if (b.n == K) {
+        b.thr = b.d[64 * (K - 1)];
+        b.thr_leaf = b.leaf[64 * (K - 1)];
+    }
 }
 
 template <int K>
@@ -420,6 +446,120 @@ __device__ __forceinline__ int32_t traverse_pass(const Ray& r, const float4_t* _
         }
     }
     return ncand;
+}
+
+// Near-first pass (incoherent bounce rays; LDS leaf buffer): the same leaf set as traverse_pass --
+// every inner child is still examined with the reference's per-node child loop and 5-hit limit
+// (examine_inner) -- but a node's inner children are descended in the order the ray crosses them:
+// with the child index mirrored by the direction signs (i ^ sm, sm = x, y, z sign bits), the
+// octants a line crosses have increasing mirrored indices (each plane crossing sets one more bit),
+// so the per-level mask is kept mirrored and popped lowest bit first. The nearest leaves then
+// fill the K-entry buffer first, and once it is full a subtree whose entry distance exceeds its
+// K-th distance is skipped: every leaf below it has a distance >= that entry (nested octant boxes,
+// monotone f32 slab values; a leaf the origin lies in has dis = its exit > 0 >= its entry), so
+// none could enter the buffer. Skipping makes the candidate count a lower bound, so a pass that
+// skipped anything reports more than K candidates (the ray re-walks after its K leaves, as a pass
+// with more than K candidates does). Leaves are discovered out of rank order: the buffer keeps
+// (distance, rank) order (lb_insert_lex). Skips only with finite 1/d on every axis (no NaN slabs).
+template <int K, bool COUNT>
+__device__ __forceinline__ uint32_t examine_near(const Ray& r, const Inner& n, LdsLeafBuf<K>& lb, int32_t& ncand,
+                                                 float bd, int32_t bi, Ctr& ct, bool first_pass, bool cull,
+                                                 uint32_t sm, bool& skipped) {
+    const float X0 = (n.lx - r.o.x) * r.inv.x, X1 = (n.vx - r.o.x) * r.inv.x, X2 = (n.hx - r.o.x) * r.inv.x;
+    const float Y0 = (n.ly - r.o.y) * r.inv.y, Y1 = (n.vy - r.o.y) * r.inv.y, Y2 = (n.hy - r.o.y) * r.inv.y;
+    const float Z0 = (n.lz - r.o.z) * r.inv.z, Z1 = (n.vz - r.o.z) * r.inv.z, Z2 = (n.hz - r.o.z) * r.inv.z;
+    const float nx0 = r.s0 ? X1 : X0, nx1 = r.s0 ? X2 : X1, fx0 = r.s0 ? X0 : X1, fx1 = r.s0 ? X1 : X2;
+    const float ny0 = r.s1 ? Y1 : Y0, ny1 = r.s1 ? Y2 : Y1, fy0 = r.s1 ? Y0 : Y1, fy1 = r.s1 ? Y1 : Y2;
+    const float nz0 = r.s2 ? Z1 : Z0, nz1 = r.s2 ? Z2 : Z1, fz0 = r.s2 ? Z0 : Z1, fz1 = r.s2 ? Z1 : Z2;
+    const bool full = cull && lb.n == K;
+    uint32_t mask = 0;
+    int nodes_hit = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (nodes_hit > 4) break;
+        if constexpr (COUNT) { ct.box_all += 1; ct.box += first_pass ? 1u : 0u; }
+        float tmin = (i >> 2) ? nx1 : nx0, tmax = (i >> 2) ? fx1 : fx0;
+        const float tymin = ((i >> 1) & 1) ? ny1 : ny0, tymax = ((i >> 1) & 1) ? fy1 : fy0;
+        const float tzmin = (i & 1) ? nz1 : nz0, tzmax = (i & 1) ? fz1 : fz0;
+        bool in = !((tmin > tymax) || (tymin > tmax));
+        if (tymin > tmin) tmin = tymin;
+        if (tymax < tmax) tmax = tymax;
+        in = in && !((tmin > tzmax) || (tzmin > tmax));
+        if (!((n.bm >> i) & 1u)) {  // inner child: check_ray_AABB_intersection (aabb.h:65-93)
+            if (in) {
+                ++nodes_hit;
+                const float tx = tzmax < tmax ? tzmax : tmax;
+                const float tn = tzmin > tmin ? tzmin : tmin;  // its entry distance (z merged)
+                if (cull && (tx <= 0.0f || tx < bd)) continue;  // behind the origin or the re-walk bound
+                if (full && tn > lb.thr) { skipped = true; continue; }
+                mask |= 1u << (i ^ int(sm));
+            }
+        } else {  // leaf child: get_ray_AABB_intersection (aabb.h:29-63)
+            if (tzmin > tmin) tmin = tzmin;
+            if (tzmax < tmax) tmax = tzmax;
+            const float dis = !in ? 0.0f : (tmin > 0 ? tmin : (tmax > 0 ? tmax : 0.0f));
+            if (dis > 0.0f) {
+                ++nodes_hit;
+                const int32_t id = n.leaf0 + __popc(n.bm & ((1u << i) - 1u) & 0xFFu);
+                if (dis > bd || (dis == bd && id > bi)) {
+                    ++ncand;
+                    lb_insert_lex<K>(lb, dis, id);
+                }
+            }
+        }
+    }
+    return mask;
+}
+
+template <int K, bool COUNT>
+__device__ __forceinline__ int32_t traverse_pass_near(const Ray& r, const float4_t* __restrict__ tab,
+                                                      LdsLeafBuf<K>& lb, float bd, int32_t bi, Ctr& ct) {
+    const bool first_pass = bi < 0;
+    if constexpr (COUNT) ct.pass += 1;
+    lb_clear<K>(lb);
+    int32_t ncand = 0;
+    const bool cull = isfinite(r.inv.x) && isfinite(r.inv.y) && isfinite(r.inv.z);
+    const uint32_t sm = (uint32_t(r.s0) << 2) | (uint32_t(r.s1) << 1) | uint32_t(r.s2);
+    bool skipped = false;
+    Inner cur = load_inner(tab, 0);
+    uint64_t lo = examine_near<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull, sm, skipped);
+    uint64_t hi = 0;
+    uint32_t bm = cur.bm;
+    int32_t parent = -1, lvl = 0;
+    for (;;) {
+        if constexpr (COUNT) { ct.node_wave += first_active_lane(); ct.node_lane += 1; }
+        const uint32_t m = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
+        if (m) {
+            const int sb = __builtin_ctz(m);  // nearest remaining child (mirrored index)
+            if (lvl < 8) lo &= ~(uint64_t(1) << (8 * lvl + sb));
+            else hi &= ~(uint64_t(1) << (8 * (lvl - 8) + sb));
+            const int s = sb ^ int(sm);
+            const uint32_t innerm = ~bm & ((1u << s) - 1u);  // inner children before s
+            const int32_t id = int32_t(bm >> 8) + __popc(innerm);
+            cur = load_inner(tab, id);
+            if (cull && lb.n == K) {  // the buffer filled since this child was pushed: its entry
+                const float ex = r.s0 ? (cur.hx - r.o.x) * r.inv.x : (cur.lx - r.o.x) * r.inv.x;
+                const float ey = r.s1 ? (cur.hy - r.o.y) * r.inv.y : (cur.ly - r.o.y) * r.inv.y;
+                const float ez = r.s2 ? (cur.hz - r.o.z) * r.inv.z : (cur.lz - r.o.z) * r.inv.z;
+                const float txy = ey > ex ? ey : ex;
+                if ((ez > txy ? ez : txy) > lb.thr) { skipped = true; continue; }
+            }
+            const uint64_t cm = examine_near<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull, sm, skipped);
+            ++lvl;
+            if (lvl >= kMaskLevels) return -1;
+            if (lvl < 8) lo |= cm << (8 * lvl);
+            else hi |= cm << (8 * (lvl - 8));
+            bm = cur.bm;
+            parent = cur.parent;
+        } else {
+            if (lvl == 0) break;
+            --lvl;
+            const float4_t t = tab[3 * parent + 2];
+            bm = __float_as_uint(t.w);
+            parent = __float_as_int(t.z);
+        }
+    }
+    return skipped && ncand <= K ? K + 1 : ncand;
 }
 
 // The same pass walked by the whole wavefront (coherent primary rays): the wave visits the union
