@@ -1135,6 +1135,11 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
             dm.tris = static_cast<const DTri*>(p);
             dm.has_tree = 1;
             dm.root_leaf = T.children[0] == 0;
+            {
+                int32_t depth = 0;
+                for (int32_t d : T.depth) depth = std::max(depth, d);
+                dm.near_ok = depth <= 8 && dm.ninner < 65536;  // traverse_pass_near's register stack
+            }
             if (T.nnodes > c->max_nodes) c->max_nodes = T.nnodes;
         } else {  // brute force: face-ordered triangles straight from the mesh (renderer.cpp:61-66)
             std::vector<DTri> tris(nf);

@@ -136,6 +136,7 @@ struct DModel {
     uint32_t nfaces;
     int32_t has_tree;
     int32_t root_leaf;           // root never split (kd_tree.cpp:344-361)
+    int32_t near_ok;             // depth <= 8 and < 2^16 inner nodes: near-first passes (trace.h)
     int32_t smooth;              // normals.size > 0 (renderer.cpp:129)
     int32_t material;
     float aabb[6];               // Model::surrounding_aabb

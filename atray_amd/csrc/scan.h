@@ -308,7 +308,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                 LdsLeafBuf<K> lb;
                 lb.d = &s_lbd[w][0][ln];
                 lb.leaf = &s_lbl[w][0][ln];
-                if constexpr (NEAR) n = traverse_pass_near<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+                if (NEAR && m.near_ok) n = traverse_pass_near<K, COUNT>(r, m.inner, lb, bd, bi, ct);
                 else n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
             } else {  // register buffer: the LDS one measured 5% slower for incoherent bounce rays
                 LeafBuf<K> lb;

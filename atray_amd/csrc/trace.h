@@ -511,6 +511,14 @@ __device__ __forceinline__ uint32_t examine_near(const Ray& r, const Inner& n, L
     return mask;
 }
 
+// The pass's stack lives in registers, one 32-bit entry per level: the level's remaining inner
+// children (mirrored mask, bits 0-7), the node's leaf-children mask (8-15) and its first inner
+// child's id (16-31) -- everything a pop needs, so an ascent is a register shift and every loop
+// iteration is one descent (the mask stack of traverse_pass re-reads the parent's record on each
+// ascent: a dependent load per level climbed). A node with no inner child to visit is not pushed.
+// Holds kNearLevels levels (four u64, the top entry in the low half of s0); trees deeper than that,
+// or with 2^16 or more inner nodes, take traverse_pass (DModel::near_ok, set at upload).
+constexpr int kNearLevels = 8;
 template <int K, bool COUNT>
 __device__ __forceinline__ int32_t traverse_pass_near(const Ray& r, const float4_t* __restrict__ tab,
                                                       LdsLeafBuf<K>& lb, float bd, int32_t bi, Ctr& ct) {
@@ -522,41 +530,41 @@ __device__ __forceinline__ int32_t traverse_pass_near(const Ray& r, const float4
     const uint32_t sm = (uint32_t(r.s0) << 2) | (uint32_t(r.s1) << 1) | uint32_t(r.s2);
     bool skipped = false;
     Inner cur = load_inner(tab, 0);
-    uint64_t lo = examine_near<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull, sm, skipped);
-    uint64_t hi = 0;
-    uint32_t bm = cur.bm;
-    int32_t parent = -1, lvl = 0;
+    const uint32_t m0 = examine_near<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull, sm, skipped);
+    uint64_t s0 = m0 ? uint64_t(m0 | ((cur.bm & 0xFFu) << 8) | ((cur.bm >> 8) << 16)) : 0, s1 = 0, s2 = 0, s3 = 0;
+    int32_t depth = m0 ? 1 : 0;
     for (;;) {
+        while (depth > 0 && (uint32_t(s0) & 0xFFu) == 0) {  // ascend: pop the exhausted levels
+            s0 = (s0 >> 32) | (s1 << 32);
+            s1 = (s1 >> 32) | (s2 << 32);
+            s2 = (s2 >> 32) | (s3 << 32);
+            s3 >>= 32;
+            --depth;
+        }
+        if (depth == 0) break;
         if constexpr (COUNT) { ct.node_wave += first_active_lane(); ct.node_lane += 1; }
-        const uint32_t m = lvl < 8 ? uint32_t(lo >> (8 * lvl)) & 0xFFu : uint32_t(hi >> (8 * (lvl - 8))) & 0xFFu;
-        if (m) {
-            const int sb = __builtin_ctz(m);  // nearest remaining child (mirrored index)
-            if (lvl < 8) lo &= ~(uint64_t(1) << (8 * lvl + sb));
-            else hi &= ~(uint64_t(1) << (8 * (lvl - 8) + sb));
-            const int s = sb ^ int(sm);
-            const uint32_t innerm = ~bm & ((1u << s) - 1u);  // inner children before s
-            const int32_t id = int32_t(bm >> 8) + __popc(innerm);
-            cur = load_inner(tab, id);
-            if (cull && lb.n == K) {  // the buffer filled since this child was pushed: its entry
-                const float ex = r.s0 ? (cur.hx - r.o.x) * r.inv.x : (cur.lx - r.o.x) * r.inv.x;
-                const float ey = r.s1 ? (cur.hy - r.o.y) * r.inv.y : (cur.ly - r.o.y) * r.inv.y;
-                const float ez = r.s2 ? (cur.hz - r.o.z) * r.inv.z : (cur.lz - r.o.z) * r.inv.z;
-                const float txy = ey > ex ? ey : ex;
-                if ((ez > txy ? ez : txy) > lb.thr) { skipped = true; continue; }
-            }
-            const uint64_t cm = examine_near<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull, sm, skipped);
-            ++lvl;
-            if (lvl >= kMaskLevels) return -1;
-            if (lvl < 8) lo |= cm << (8 * lvl);
-            else hi |= cm << (8 * (lvl - 8));
-            bm = cur.bm;
-            parent = cur.parent;
-        } else {
-            if (lvl == 0) break;
-            --lvl;
-            const float4_t t = tab[3 * parent + 2];
-            bm = __float_as_uint(t.w);
-            parent = __float_as_int(t.z);
+        const uint32_t top = uint32_t(s0);
+        const int sb = __builtin_ctz(top & 0xFFu);  // nearest remaining child (mirrored index)
+        s0 &= ~uint64_t(1u << sb);
+        const int s = sb ^ int(sm);
+        const uint32_t innerm = ~(top >> 8) & ((1u << s) - 1u) & 0xFFu;  // inner children before s
+        const int32_t id = int32_t(top >> 16) + __popc(innerm);
+        cur = load_inner(tab, id);
+        if (cull && lb.n == K) {  // the buffer filled since this child was pushed: its entry
+            const float ex = r.s0 ? (cur.hx - r.o.x) * r.inv.x : (cur.lx - r.o.x) * r.inv.x;
+            const float ey = r.s1 ? (cur.hy - r.o.y) * r.inv.y : (cur.ly - r.o.y) * r.inv.y;
+            const float ez = r.s2 ? (cur.hz - r.o.z) * r.inv.z : (cur.lz - r.o.z) * r.inv.z;
+            const float txy = ey > ex ? ey : ex;
+            if ((ez > txy ? ez : txy) > lb.thr) { skipped = true; continue; }
+        }
+        const uint32_t cm = examine_near<K, COUNT>(r, cur, lb, ncand, bd, bi, ct, first_pass, cull, sm, skipped);
+        if (cm) {  // push the node's level
+            if (depth >= kNearLevels) return -1;
+            s3 = (s3 << 32) | (s2 >> 32);
+            s2 = (s2 << 32) | (s1 >> 32);
+            s1 = (s1 << 32) | (s0 >> 32);
+            s0 = (s0 << 32) | uint64_t(cm | ((cur.bm & 0xFFu) << 8) | ((cur.bm >> 8) << 16));
+            ++depth;
         }
     }
     return skipped && ncand <= K ? K + 1 : ncand;
