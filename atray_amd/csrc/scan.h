@@ -268,9 +268,12 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
-    bool done = true, need = false, more = false;
-    int32_t j = 0, nb = 0, bi = -1;
-    float bd = -__builtin_inff();
+    // the re-walk bound (bd, bi) is the last leaf of the previous pass's full buffer (entry K - 1 of
+    // the LDS column), read when the pass starts; the ray's result stays in its LDS key/slot/u/v
+    // row once it is done (no register holds it through the scan)
+    bool done = true, need = false, more = false, rewalk = false;
+    int32_t j = 0, nb = 0;
+    s_key[w][ln] = kKeyInit;
     if (active) {
         const NodeBox root = load_node(m.nodes, 0);
         if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
@@ -285,10 +288,10 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             }
         }
     }
-    uint32_t res_slot = 0xFFFFFFFFu;
-    float res_t = kMaxFloat, res_u = 0.f, res_v = 0.f;
     for (;;) {
         ATR_PCLK(const uint64_t tc0 = clock64());
+        const float bd = rewalk ? s_lbd[w][K - 1][ln] : -__builtin_inff();
+        const int32_t bi = rewalk ? s_lbl[w][K - 1][ln] : -1;
         if constexpr (UT) {  // the wave walks its passes together (traverse_pass_wave)
             if (__ballot(need)) {
                 LdsLeafBuf<K> lb;
@@ -326,11 +329,9 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         const uint64_t livem = __ballot(!done);
         if (livem == 0) break;
         // every live ray's current leaf: its clusters are this step's items
-        int32_t leaf = -1;
         uint32_t cf = 0, cn = 0;
         if (!done) {
-            leaf = s_lbl[w][j][ln];
-            const uint2_t cr = load_range(m.cl_range, leaf);
+            const uint2_t cr = load_range(m.cl_range, s_lbl[w][j][ln]);
             cf = cr.x;
             cn = cr.y;
             if constexpr (COUNT) { ct.leaf += 1; ct.cbox += cn; }
@@ -338,7 +339,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         const uint32_t incl = wave_incl_add(cn);  // inclusive prefix sum over the lanes
         const uint32_t excl = incl - cn;
         const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
-        s_key[w][ln] = kKeyInit;
+        if (!done) s_key[w][ln] = kKeyInit;
         bool deal = true;
         if constexpr (HYB) {
             // the largest cluster count of the step (counts are small: the signed max is exact)
@@ -393,31 +394,23 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
         }
         ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
         if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
-            const unsigned long long key = s_key[w][ln];
-            if (key != kKeyInit) {
-                res_t = __uint_as_float(uint32_t(key >> 32));
-                res_slot = s_slot[w][ln];
-                if constexpr (!NUV) {
-                    res_u = s_u[w][ln];
-                    res_v = s_v[w][ln];
-                }
+            if (s_key[w][ln] != kKeyInit) {
                 done = true;
-            } else {
-                bd = s_lbd[w][j][ln];
-                bi = leaf;
-                if (++j >= nb) {
-                    if (more) need = true;
-                    else done = true;
-                }
+            } else if (++j >= nb) {
+                if (more) need = rewalk = true;  // the next K leaves after this buffer's last
+                else done = true;
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (res_slot != 0xFFFFFFFFu) {
-        h.t = res_t;
-        h.u = res_u;
-        h.v = res_v;
-        h.face = m.cface[res_slot];
+    const unsigned long long key = s_key[w][ln];
+    if (active && key != kKeyInit) {
+        h.t = __uint_as_float(uint32_t(key >> 32));
+        if constexpr (!NUV) {
+            h.u = s_u[w][ln];
+            h.v = s_v[w][ln];
+        }
+        h.face = m.cface[s_slot[w][ln]];
     }
     ATR_PCLK(ct.t_scan += uint32_t(clock64() - tcs));
 }
