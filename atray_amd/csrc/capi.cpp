@@ -1064,9 +1064,8 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 // the record's last word can carry the screen normals' step instead
                 const size_t ncl = C.rec.size() / 8;
                 const size_t ns = std::max<size_t>(1, ncl) * kMaxClusterSize;
-                std::vector<float4_t> s0(ns, float4_t{0.f, 0.f, 0.f, 0.f}), s1(ns, float4_t{0.f, 0.f, 0.f, 0.f});
-                std::vector<c2_t> s2(ns, c2_t{});
-                std::vector<uint32_t> sf(ns, 0u);
+                // full-test records, 48 B per slot (cluster.h load_prim)
+                std::vector<float4_t> pr(3 * ns, float4_t{0.f, 0.f, 0.f, 0.f});
                 // screen normals, 24 u32 per cluster: (nx, ny) of slot k as f16 in word k, then
                 // (nz of slot 2i, nz of slot 2i + 1) in word 16 + i (cluster.h)
                 std::vector<uint32_t> nw(std::max<size_t>(1, ncl) * 24, 0u);
@@ -1088,13 +1087,12 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                     for (uint32_t i = 0; i < n; ++i) {
                         const size_t k = first + i, slot = cl * kMaxClusterSize + i;
                         const DTri& t = tris[C.order[k]];
-                        s0[slot] = float4_t{t.ax, t.ay, t.az, t.abx};
-                        s1[slot] = float4_t{t.aby, t.abz, t.acx, t.acy};
-                        float rk;
+                        float rk, fc;
                         std::memcpy(&rk, &C.rank[k], 4);
-                        s2[slot].x = t.acz;
-                        s2[slot].y = rk;
-                        sf[slot] = t.face;
+                        std::memcpy(&fc, &t.face, 4);
+                        pr[3 * slot] = float4_t{t.ax, t.ay, t.az, t.abx};
+                        pr[3 * slot + 1] = float4_t{t.aby, t.abz, t.acx, t.acy};
+                        pr[3 * slot + 2] = float4_t{t.acz, rk, fc, 0.f};
                         uint16_t h[3];
                         for (int a = 0; a < 3; ++a) {
                             long v = std::lround(double(C.normal[3 * k + a]) / double(q));
@@ -1117,14 +1115,8 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 C.range = by_rank(C.range);
                 if ((rc = dev_upload(c, C.range.data(), C.range.size() * sizeof(uint32_t), &p))) return rc;
                 dm.cl_range = static_cast<const uint32_t*>(p);
-                if ((rc = dev_upload(c, s0.data(), s0.size() * sizeof(float4_t), &p))) return rc;
-                dm.c0 = static_cast<const float4_t*>(p);
-                if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
-                dm.c1 = static_cast<const float4_t*>(p);
-                if ((rc = dev_upload(c, s2.data(), s2.size() * sizeof(c2_t), &p))) return rc;
-                dm.c2 = static_cast<const c2_t*>(p);
-                if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
-                dm.cface = static_cast<const uint32_t*>(p);
+                if ((rc = dev_upload(c, pr.data(), pr.size() * sizeof(float4_t), &p))) return rc;
+                dm.prim = static_cast<const float4_t*>(p);
                 c->nclusters += int64_t(ncl);
             }
             if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;

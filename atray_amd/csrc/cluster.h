@@ -40,40 +40,13 @@ struct LeafHit {
     bool improved;
 };
 
-template <bool COUNT>
-__device__ __forceinline__ void cluster_tri_test(const Ray& r, float4_t q0, float4_t q1, c2_t q2, uint32_t k,
-                                                 LeafHit& h, Ctr& ct) {
-    if constexpr (COUNT) ct.tri += 1;
-    float u = 0.f, v = 0.f;
-    const float dist = tri_hit(r, mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), mk(q1.z, q1.w, q2.x), u, v);
-    if (dist <= h.t && dist > kTol) {
-        const int32_t rk = __float_as_int(q2.y);
-        if (dist < h.t || (h.rank >= 0 && rk < h.rank)) {
-            h.t = dist;
-            h.slot = k;
-            h.u = u;
-            h.v = v;
-            h.rank = rk;
-            h.improved = true;
-        }
-    }
-}
-
-// The full-test operands of slot k: a, ab, ac and the leaf rank (c2.y). (64-B slot records, one
-// cache line per test, measured no faster once the candidates are compacted: DESIGN.md §4f.)
-__device__ __forceinline__ void load_prim(const DModel& m, uint32_t k, float4_t& a0, float4_t& a1, c2_t& a2) {
-    a0 = m.c0[k];
-    a1 = m.c1[k];
-    a2 = m.c2[k];
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void cluster_tri(const Ray& r, const DModel& m, uint32_t k, LeafHit& h,
-                                            Ctr& ct) {
-    float4_t a0, a1;
-    c2_t a2;
-    load_prim(m, k, a0, a1, a2);
-    cluster_tri_test<COUNT>(r, a0, a1, a2, k, h, ct);
+// The full-test operands of slot k, one 48-B record {a.xyz, ab.x}{ab.yz, ac.xy}{ac.z, bits(leaf
+// rank), bits(face), 0}: one cache line (at most two) per test. (Round 3's three SoA streams
+// touched three lines per test; incoherent bounce rays miss in L2 on most of them)
+__device__ __forceinline__ void load_prim(const DModel& m, uint32_t k, float4_t& a0, float4_t& a1, float4_t& a2) {
+    a0 = m.prim[3 * size_t(k)];
+    a1 = m.prim[3 * size_t(k) + 1];
+    a2 = m.prim[3 * size_t(k) + 2];
 }
 
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
@@ -192,63 +165,6 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
         cand |= screen8(sr, blo, ahi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8]) << g;
     return cand & slots;
-}
-
-// Cluster c of the current leaf (lane-private schedule): padded box tests, then the screen and
-// the full tests of its primitives.
-template <bool COUNT, bool PAIR = false>
-__device__ __forceinline__ void cluster_step(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
-                                             LeafHit& h, Ctr& ct) {
-    uint32_t cand = cluster_cands<COUNT>(r, m, c, lo, hi, h.t, ct);
-    const uint32_t first = kMaxClusterSize * c;
-    if constexpr (!PAIR) {
-        // one at a time: the lane-private CLUSTER kernel's peak stays at 94 VGPRs (no scratch at
-        // 5 waves/SIMD); two in flight measured slower there
-        while (cand) {
-            if constexpr (COUNT) ct.cand_wave += first_active_lane();
-            const uint32_t k = first + uint32_t(__builtin_ctz(cand));
-            cand &= cand - 1;
-            cluster_tri<COUNT>(r, m, k, h, ct);
-        }
-    } else {
-        while (cand) {  // two primitives' loads in flight (FLAT: faster despite the registers)
-            if constexpr (COUNT) ct.cand_wave += first_active_lane();
-            const uint32_t ka = first + uint32_t(__builtin_ctz(cand));
-            cand &= cand - 1;
-            float4_t a0, a1;
-            c2_t a2;
-            load_prim(m, ka, a0, a1, a2);
-            if (cand) {
-                const uint32_t kb = first + uint32_t(__builtin_ctz(cand));
-                cand &= cand - 1;
-                float4_t b0, b1;
-                c2_t b2;
-                load_prim(m, kb, b0, b1, b2);
-                cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
-                cluster_tri_test<COUNT>(r, b0, b1, b2, kb, h, ct);
-            } else {
-                cluster_tri_test<COUNT>(r, a0, a1, a2, ka, h, ct);
-            }
-        }
-    }
-}
-
-// Clusters [c, cend) of one leaf, the next cluster's record in flight while the current one is
-// screened (the record shares its 128-B block with the cluster's screen normals, so that load
-// also brings the normals the screen reads next).
-template <bool COUNT>
-__device__ __forceinline__ void cluster_range(const Ray& r, const DModel& m, uint32_t c, uint32_t cend, LeafHit& h,
-                                              Ctr& ct) {
-    if (c >= cend) return;
-    float4_t nlo = m.clus[kClusterBlock * size_t(c)], nhi = m.clus[kClusterBlock * size_t(c) + 1];
-    for (; c < cend; ++c) {
-        const float4_t lo = nlo, hi = nhi;
-        if (c + 1 < cend) {
-            nlo = m.clus[kClusterBlock * size_t(c + 1)];
-            nhi = m.clus[kClusterBlock * size_t(c + 1) + 1];
-        }
-        cluster_step<COUNT>(r, m, c, lo, hi, h, ct);
-    }
 }
 
 }  // namespace atr

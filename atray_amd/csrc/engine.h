@@ -21,11 +21,6 @@ struct alignas(16) float4_t { float x, y, z, w; };
 struct alignas(16) uint4_t { uint32_t x, y, z, w; };
 struct alignas(8) float2_t { float x, y; };
 struct alignas(8) uint2_t { uint32_t x, y; };
-#ifdef ATR_C2_WIDE
-using c2_t = float4_t;  // experiment: 16-B third word
-#else
-using c2_t = float2_t;
-#endif
 
 constexpr float kMaxFloat = 3.402823466e+38F;     // PL_base_defs.h:72
 constexpr float kInvU32Max = 2.328306437e-10F;    // PL_base_defs.h:75
@@ -123,15 +118,12 @@ struct DModel {
     // (n - 1) in its low 5 mantissa bits}, {hi.xyz, q}; cl_range = first cluster, count per
     // node. Cluster c owns the primitive slots [16 c, 16 c + n) and the 128-B block clus[8 c ..]:
     // its record (2 words), then (cnrm = clus + 2) 6 words of its screen normals
-    // n = ab x ac as f16 integer multiples of q (the screen, cluster.h), c0 = {a.xyz, ab.x},
-    // c1 = {ab.yz, ac.xy}, c2 = {ac.z, bits(leaf rank)}, cface = face index
+    // n = ab x ac as f16 integer multiples of q (the screen, cluster.h); prim = 48 B per slot:
+    // {a.xyz, ab.x}{ab.yz, ac.xy}{ac.z, bits(leaf rank), bits(face index), 0}
     const float4_t* clus;
     const uint32_t* cl_range;
     const uint4_t* cnrm;
-    const float4_t* c0;
-    const float4_t* c1;
-    const c2_t* c2;
-    const uint32_t* cface;
+    const float4_t* prim;
     const float* shade;          // 9 f32 per face: smooth -> na, nb, nc; flat -> v0, v1, v2
     uint32_t nfaces;
     int32_t has_tree;

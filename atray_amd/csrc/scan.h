@@ -216,7 +216,7 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
         if (valid) {
             if constexpr (COUNT) { ct.tri += 1; ct.cand_wave += ln == 0 ? 1u : 0u; }
             float4_t a0, a1;
-            c2_t a2;
+            float4_t a2;
             load_prim(m, slot, a0, a1, a2);
             const float dist = tri_hit(q, mk(a0.x, a0.y, a0.z), mk(a0.w, a1.x, a1.y), mk(a1.z, a1.w, a2.x), u, v);
             if (dist > kTol && dist < kMaxFloat) {  // accepted (model.h:75-103; kd_tree.cpp:450)
@@ -410,7 +410,7 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
             h.u = s_u[w][ln];
             h.v = s_v[w][ln];
         }
-        h.face = m.cface[s_slot[w][ln]];
+        h.face = __float_as_uint(m.prim[3 * size_t(s_slot[w][ln]) + 2].z);
     }
     ATR_PCLK(ct.t_scan += uint32_t(clock64() - tcs));
 }
@@ -438,10 +438,7 @@ __device__ __forceinline__ DModel uniform_model(const DModel& src) {
     m.clus = uniform_global(m.clus);
     m.cl_range = uniform_global(m.cl_range);
     m.cnrm = uniform_global(m.cnrm);
-    m.c0 = uniform_global(m.c0);
-    m.c1 = uniform_global(m.c1);
-    m.c2 = uniform_global(m.c2);
-    m.cface = uniform_global(m.cface);
+    m.prim = uniform_global(m.prim);
     return m;
 }
 

@@ -1,6 +1,7 @@
 #!/bin/bash
-# PMC passes over tools/pmc_probe.py, one counter group per rocprofv3 run (--kernel-trace only),
-# each under its own time limit. Output: gpurun_out/pmc2/g<i>/..., summarized by tools/pmc_summary2.py.
+# PMC passes over a probe (PROBE, default tools/pmc_probe.py; e.g. PROBE="tools/path_probe.py c4 0 1"),
+# one counter group per rocprofv3 run (--kernel-trace only), each under its own time limit.
+# Output: gpurun_out/$OUT_DIR/g<i>/..., summarized by tools/pmc_summary2.py.
 export TMPDIR=/tmp
 O=gpurun_out/${OUT_DIR:-pmc2}
 mkdir -p $O
@@ -8,7 +9,7 @@ i=0
 while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $O/g$i -o p -- python3 tools/pmc_probe.py > $O/g$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $O/g$i -o p -- python3 ${PROBE:-tools/pmc_probe.py} > $O/g$i.log 2>&1
   rc=$?; echo "group $i ($grp) rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done <<'GROUPS'
@@ -20,6 +21,7 @@ TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum
 TD_TD_BUSY_sum TD_TC_STALL_sum
 GRBM_GUI_ACTIVE SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH
 TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_READ_sum TCP_TOTAL_WRITE_sum TCP_TCC_WRITE_REQ_sum
+SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SALU SQ_WAVES
 FETCH_SIZE
 WRITE_SIZE
 GROUPS
