@@ -492,7 +492,7 @@ __device__ __forceinline__ uint32_t examine_near(const Ray& r, const Inner& n, L
                 const float tn = tzmin > tmin ? tzmin : tmin;  // its entry distance (z merged)
                 if (cull && (tx <= 0.0f || tx < bd)) continue;  // behind the origin or the re-walk bound
                 if (full && tn > lb.thr) { skipped = true; continue; }
-                mask |= 1u << (i ^ int(sm));
+                mask |= 1u << i;
             }
         } else {  // leaf child: get_ray_AABB_intersection (aabb.h:29-63)
             if (tzmin > tmin) tmin = tzmin;
@@ -508,6 +508,11 @@ __device__ __forceinline__ uint32_t examine_near(const Ray& r, const Inner& n, L
             }
         }
     }
+    // bit i -> bit i ^ sm, mirrored once here (per-child shifts by (i ^ sm) were hoisted out of the
+    // pass loop as eight per-lane constants, and spilled)
+    if (sm & 4u) mask = ((mask & 0x0Fu) << 4) | ((mask & 0xF0u) >> 4);
+    if (sm & 2u) mask = ((mask & 0x33u) << 2) | ((mask & 0xCCu) >> 2);
+    if (sm & 1u) mask = ((mask & 0x55u) << 1) | ((mask & 0xAAu) >> 1);
     return mask;
 }
 

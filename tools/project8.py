@@ -4,13 +4,13 @@ full-frame ms per frame / slowest shard's; the exchange adds rank 0's receive of
 3-byte pixels, (1 - share_0) x W x H x 3 B per frame, at an assumed xGMI rate into rank 0, either
 fully exposed or exposed only for the last launch of each stream (the stream-priority overlap,
 DESIGN.md §5), plus rank 0's scatter into BGRX images (HBM-bound: 3 B read + 4 B written per pixel
-at 5 TB/s). Usage: python tools/project8.py [xgmi GB/s ...] > profiles/r03/projection8.json"""
+at 5 TB/s). Usage: PROFILE=profiles/r04 python tools/project8.py [xgmi GB/s ...] > profiles/r04/projection8.json"""
 import json
 import os
 import sys
 
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sim = json.load(open(os.path.join(R, "profiles", "r03", "sim8_shards.json")))
+sim = json.load(open(os.path.join(R, os.environ.get("PROFILE", "profiles/r04"), "sim8_shards.json")))
 rates = [float(x) for x in sys.argv[1:]] or [200.0, 350.0, 500.0]
 PIX = {"c3": 1920 * 1080, "c4": 1920 * 1080, "c5": 3840 * 2160}
 out = {"assumptions": {"xgmi_gbs_into_rank0": rates, "scatter_tbs": 5.0, "bytes_per_pixel": 3}, "configs": {}}
