@@ -25,7 +25,7 @@
 
 using namespace atr;
 
-extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int wave, hipStream_t s);
+extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, int primary_occ, hipStream_t s);
 extern "C" hipError_t atr_launch_traced_finish(unsigned long long* slots, unsigned long long* out, hipStream_t s);
 extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                         const uint32_t* packed, uint32_t* image, hipStream_t s);
@@ -571,7 +571,7 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
 
 hipError_t launch_kernels(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
     if (sched == kSchedPaths) return launch_paths(c, P, s);
-    return atr_launch_render(P, sched, s);
+    return atr_launch_render(P, sched, c->tune.primary_occ, s);
 }
 
 // Launch a render schedule; the traced rays go into a zeroed set of 64 spread counters from the
@@ -875,7 +875,8 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
         t->hybrid_a < -4096 || t->hybrid_a > 4096 || t->hybrid_b < -4096 || t->hybrid_b > 4096 ||
         t->path_batch_log2 < 12 || t->path_batch_log2 > 30 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
         t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
-        (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)))
+        (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)) ||
+        (t->primary_occ != 0 && t->primary_occ != 6 && t->primary_occ != 7))
         return ATR_E_INVALID;
     for (int32_t r : t->reserved)
         if (r) return ATR_E_INVALID;
@@ -1372,7 +1373,7 @@ int atr_render_wave_trace(atr_ctx* c, const atr_camera* cam, const atr_tile* til
     P.wave_trace = static_cast<unsigned long long*>(tr.p);
     apply_tuning(c, P);
     const int ts = sched_of(variant);  // per-cell trace: 8x8-cell schedules only
-    HIPCHK(atr_launch_render(P, ts < 0 || ts == kSchedPaths ? 7 : ts, nullptr));
+    HIPCHK(atr_launch_render(P, ts < 0 || ts == kSchedPaths ? 7 : ts, 0, nullptr));
     HIPCHK(hipDeviceSynchronize());
     if (nb) HIPCHK(hipMemcpy(out, tr.p, 3 * nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return ATR_OK;

@@ -365,19 +365,20 @@ static void launch_one(const atr::RenderParams& P, hipStream_t s) {
 
 // sched: 0 LANE, 6 FLAT, 7 HYBRID (capi.cpp sched_of). Occupancy per schedule and launch shape by
 // measurement: one frame at 6 waves/SIMD (its slowest cells set the latency),
-// frames in flight at 7 (throughput).
-extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, hipStream_t s) {
+// frames in flight at 7 (throughput); primary_occ 6 / 7 overrides the HYBRID primary choice.
+extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, int primary_occ, hipStream_t s) {
     using namespace atr;
     if (P.nblocks <= 0) return hipSuccess;
     if (P.traced_rays && P.counters) return hipErrorInvalidValue;  // traced_rays is a ring slot (engine.h)
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing && P.cam.samples_per_pixel == 1;
     const bool multi = P.frame_blocks > 0;
+    const bool prim7 = primary_occ ? primary_occ == 7 : multi;
     switch (sched) {
         case SCHED_HYBRID:
             if (count) { if (prim) launch_one<SCHED_HYBRID, true, true>(P, s); else launch_one<SCHED_HYBRID, true, false>(P, s); }
             else if (!prim) launch_one<SCHED_HYBRID, false, false>(P, s);  // LDS: 4 workgroups per CU
-            else if (multi) launch_one<SCHED_HYBRID, false, true, 7>(P, s);
+            else if (prim7) launch_one<SCHED_HYBRID, false, true, 7>(P, s);
             else launch_one<SCHED_HYBRID, false, true, 6>(P, s);
             break;
         case SCHED_FLAT:
