@@ -83,13 +83,15 @@ for f in ("pytest_gpu.log", "smoke.log"):
     if os.path.exists(f"{G}/r4final/{f}"):
         lines = open(f"{G}/r4final/{f}").read().strip().splitlines()
         open(f"{P}/{f.replace('.log', '_tail.txt')}", "w").write("\n".join(lines[-3:]) + "\n")
+FPL = {"trace_c3_driver": 10, "trace_c4": 4}  # frames per timed launch of the traced command
 for d in glob.glob(f"{G}/r4final/trace_*"):
     if os.path.isdir(d):
         tag = os.path.basename(d)
         for f in glob.glob(f"{d}/**/*kernel_stats.csv", recursive=True):
             shutil.copy(f, f"{P}/{tag}_kernel_stats.csv")
         with open(f"{P}/{tag}_summary.json", "w") as fh:
-            subprocess.run([sys.executable, f"{R}/tools/trace_summary.py", d], stdout=fh, check=True)
+            subprocess.run([sys.executable, f"{R}/tools/trace_summary.py", d, str(FPL.get(tag, 4)),
+                            f"{P}/{tag}_kernel_stats.csv"], stdout=fh, check=True)
 
 sim = json.load(open(f"{P}/sim8_shards.json")) if os.path.exists(f"{P}/sim8_shards.json") else {}
 for cfg in sys.argv[1:]:

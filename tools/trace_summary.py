@@ -2,7 +2,10 @@
 and duration statistics, plus the GPU busy time (union of all kernel intervals) of the
 multi-frame launches, so a reader can check bench.py's ms_per_step against the trace.
 
-Usage: python tools/trace_summary.py <dir with *kernel_trace.csv> [frames_per_launch] > summary.json
+Usage: python tools/trace_summary.py <dir with *kernel_trace.csv or rocprofv3's *_results.db>
+           [frames_per_launch] [stats.csv] > summary.json
+(rocprofv3 of ROCm 7 writes an SQLite database by default; its `kernels` view holds the same
+dispatch rows as the CSV, and `top_kernels` the --stats table, written to stats.csv if given.)
 The bench's timed launches are the render_kernel dispatches whose grid is frames_per_launch x the
 single-frame grid; their busy union / (launches x frames_per_launch) is the trace's ms per frame
 (it includes the warmup launches of the same shape, which run the same orbit frames)."""
@@ -10,6 +13,7 @@ import collections
 import csv
 import glob
 import json
+import sqlite3
 import sys
 
 
@@ -38,6 +42,19 @@ def main():
     rows = []
     for f in sorted(glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True)):
         rows += list(csv.DictReader(open(f)))
+    for f in sorted(glob.glob(f"{root}/**/*_results.db", recursive=True)):
+        db = sqlite3.connect(f)
+        for r in db.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x, workgroup_y, "
+                            "workgroup_z, scratch_size from kernels"):
+            rows.append(dict(zip(("Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X", "Grid_Size_Y",
+                                  "Grid_Size_Z", "Workgroup_Size_X", "Workgroup_Size_Y", "Workgroup_Size_Z",
+                                  "Scratch_Size"), r)))
+        if len(sys.argv) > 3:
+            cur = db.execute("select * from top_kernels")
+            with open(sys.argv[3], "w", newline="") as fh:
+                w = csv.writer(fh)
+                w.writerow([d[0] for d in cur.description])
+                w.writerows(cur)
     groups = collections.defaultdict(list)
     for r in rows:
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
