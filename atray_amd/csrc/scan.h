@@ -239,179 +239,204 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
     }
 }
 
-// One tree query of every active lane of the wave (called by all 64 lanes, converged).
-// HYB: each leaf step decides, wave-uniformly, between the lane-private scan (every lane its own
-// leaf's clusters, one per iteration, candidates compacted; best when the rays' cluster counts are
-// alike) and the dealt rounds (best when one ray's leaf dominates): deal when the largest count
-// exceeds hyb_a x rounds + hyb_b. A leaf's result does not depend on the visiting order (minimum
-// (t, leaf rank)), so the choice changes no output bit. Without HYB every step deals (FLAT).
-// LDSB: the DFS pass inserts straight into the LDS columns instead of a register buffer copied after
-// it. UO: one origin for the whole wave (camera rays). UT: the wave walks its passes together
-// (traverse_pass_wave: coherent rays). NUV: u and v feed no output (primary-only frames). NEAR (with
-// LDSB, per-lane passes): near-first passes that skip subtrees beyond the full buffer
-// (traverse_pass_near: incoherent bounce rays).
+// The pieces of a clustered tree query (tree_closest_flat below; the path engine's bounce kernel
+// runs them in its own loop). Per lane: `done` (no query, or the query finished), `need` (a DFS pass
+// is due: the first, or a re-walk after a full buffer), j / nb / more (the current leaf of the
+// buffer, its fill, whether the pass found more than fits), `rewalk` (the buffer's last entry is the
+// next pass's bound). The result stays in the lane's LDS key/slot/u/v row (flat_result).
+
+// Start a query: the root box (kd_tree.cpp:339), the root leaf alone (:344-361) or a first pass.
+struct FlatQ {
+    int32_t j, nb;
+    bool done, need, more, rewalk;
+};
+
+template <bool COUNT>
+__device__ __forceinline__ FlatQ flat_begin(const Ray& r, const DModel& m, bool active, int w, int ln, Ctr& ct) {
+    FlatLds& L = flat_lds();
+    FlatQ q{0, 0, true, false, false, false};
+    L.key[w][ln] = kKeyInit;
+    if (active) {
+        const NodeBox root = load_node(m.nodes, 0);
+        if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
+        if (box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) {
+            q.done = false;
+            if (root.children == 0) {  // the root leaf (discovery rank 0) alone
+                L.lbl[w][0][ln] = 0;
+                L.lbd[w][0][ln] = 0.f;
+                q.nb = 1;
+            } else {
+                q.need = true;
+            }
+        }
+    }
+    return q;
+}
+
+// One DFS pass (kd_tree.cpp:363-435) for every lane with `need`; its sorted leaves wait in LDS.
+// UT: the wave walks its passes together (traverse_pass_wave: coherent rays). LDSB: the pass inserts
+// straight into the LDS columns. NEAR (with LDSB): near-first passes (traverse_pass_near).
+template <bool COUNT, bool LDSB, bool UT, bool NEAR>
+__device__ __forceinline__ void flat_pass(const Ray& r, const DModel& m, int w, int ln, FlatQ& q, int& err, Ctr& ct) {
+    constexpr int K = kLeafBuf;
+    FlatLds& L = flat_lds();
+    // the re-walk bound: the last leaf of the previous pass's full buffer (entry K - 1 of the column)
+    const float bd = q.rewalk ? L.lbd[w][K - 1][ln] : -__builtin_inff();
+    const int32_t bi = q.rewalk ? L.lbl[w][K - 1][ln] : -1;
+    auto took = [&](int32_t n) {  // the pass's leaves are the lane's buffer now
+        q.need = false;
+        q.j = 0;
+        if (n < 0) { err = 1; q.done = true; }
+        else { q.nb = n < K ? n : K; q.more = n > K; if (q.nb == 0) q.done = true; }
+    };
+    if constexpr (UT) {
+        if (__ballot(q.need)) {
+            LdsLeafBuf<K> lb;
+            lb.d = &L.lbd[w][0][ln];
+            lb.leaf = &L.lbl[w][0][ln];
+            const int32_t n = traverse_pass_wave<K, COUNT>(r, m.inner, lb, bd, bi, ct, q.need);
+            if (q.need) took(n);
+        }
+    } else if (q.need) {
+        int32_t n;
+        if constexpr (LDSB) {
+            LdsLeafBuf<K> lb;
+            lb.d = &L.lbd[w][0][ln];
+            lb.leaf = &L.lbl[w][0][ln];
+            if (NEAR && m.near_ok) n = traverse_pass_near<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+            else n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+        } else {  // register buffer: the LDS one measured 5% slower for incoherent bounce rays
+            LeafBuf<K> lb;
+            n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
+#pragma unroll
+            for (int t = 0; t < K; ++t) { L.lbd[w][t][ln] = lb.d[t]; L.lbl[w][t][ln] = lb.leaf[t]; }
+        }
+        took(n);
+    }
+}
+
+// One leaf step of every lane with `live` (a query under way whose buffer is current): the
+// clusters of each such lane's current leaf, scanned lane-private or dealt over the wave (HYB
+// decides per step, wave-uniformly: deal when the largest cluster count exceeds hyb_a x rounds +
+// hyb_b; without HYB every step deals), candidates compacted. A leaf's result does not depend on
+// the visiting order (minimum (t, leaf rank)), so the choice changes no output bit. Then each live
+// lane stops at the first leaf that improved its hit (kd_tree.cpp:457-460), moves to its next
+// leaf, or asks for a re-walk. UO: one origin for the whole wave. NUV: u and v feed no output.
+template <bool COUNT, bool HYB, bool UO, bool NUV>
+__device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, int w, int ln, bool live, FlatQ& q,
+                                               Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
+    FlatLds& L = flat_lds();
+    ATR_PCLK(const uint64_t tc2 = clock64());
+    uint32_t cf = 0, cn = 0;
+    if (live) {
+        const uint2_t cr = load_range(m.cl_range, L.lbl[w][q.j][ln]);
+        cf = cr.x;
+        cn = cr.y;
+        if constexpr (COUNT) { ct.leaf += 1; ct.cbox += cn; }
+    }
+    const uint32_t incl = wave_incl_add(cn);  // inclusive prefix sum over the lanes
+    const uint32_t excl = incl - cn;
+    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
+    if (live) L.key[w][ln] = kKeyInit;
+    bool deal = true;
+    if constexpr (HYB) {
+        // the largest cluster count of the step (counts are small: the signed max is exact)
+        const uint32_t mx = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
+        deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
+    }
+    ATR_PCLK(const uint64_t tc1 = clock64());
+    ATR_PCLK(ct.t_prep += uint32_t(tc1 - tc2));
+    if (!deal) {  // every lane scans its own leaf's clusters, one per iteration; the candidates
+                  // of each iteration are compacted over the wave
+        const uint32_t mxc = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
+        for (uint32_t i = 0; i < mxc; ++i) {
+            uint32_t cm = 0;
+            if (i < cn) {
+                const uint32_t c = cf + i;
+                const float bound = __uint_as_float(uint32_t(L.key[w][ln] >> 32));
+                cm = cluster_cands<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)],
+                                          m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
+            }
+            cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
+        }
+    }
+    ATR_PCLK(if (!deal) ct.t_lp += uint32_t(clock64() - tc1));
+    int32_t carry = -1;
+    for (uint32_t base = 0; deal && base < total; base += 64) {  // rounds of 64 items, wave-uniform
+        L.mark[w][ln] = -1;
+        __builtin_amdgcn_wave_barrier();
+        if (cn > 0 && excl >= base && excl < base + 64u) L.mark[w][excl - base] = ln;
+        __builtin_amdgcn_wave_barrier();
+        int32_t own = wave_incl_max(L.mark[w][ln]);  // latest owner starting at or before this lane
+        if (own < 0) own = carry;
+        carry = __builtin_amdgcn_readlane(own, 63);
+        const uint32_t k = base + uint32_t(ln);
+        const bool valid = k < total;
+        if constexpr (COUNT) { ct.round_wave += ln == 0 ? 1u : 0u; ct.round_items += valid ? 1u : 0u; }
+        const int32_t src = valid ? own : ln;
+        Ray qr;  // the owner's ray
+        qr.o = UO ? r.o : mk(shfl_f(r.o.x, src), shfl_f(r.o.y, src), shfl_f(r.o.z, src));
+        qr.d = mk(shfl_f(r.d.x, src), shfl_f(r.d.y, src), shfl_f(r.d.z, src));
+        qr.inv = mk(shfl_f(r.inv.x, src), shfl_f(r.inv.y, src), shfl_f(r.inv.z, src));
+        qr.s0 = qr.inv.x < 0;
+        qr.s1 = qr.inv.y < 0;
+        qr.s2 = qr.inv.z < 0;
+        const uint32_t c = uint32_t(__shfl(int(cf), src)) + (k - uint32_t(__shfl(int(excl), src)));
+        uint32_t cm = 0;
+        if (valid) {
+            const float bound = __uint_as_float(uint32_t(L.key[w][own] >> 32));
+            cm = cluster_cands<COUNT>(qr, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1],
+                                      bound, ct);
+        }
+        cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
+    }
+    ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
+    if (live) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
+        if (L.key[w][ln] != kKeyInit) {
+            q.done = true;
+        } else if (++q.j >= q.nb) {
+            if (q.more) q.need = q.rewalk = true;  // the next K leaves after this buffer's last
+            else q.done = true;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The lane's result from its LDS row (t = kMaxFloat: no hit).
+template <bool NUV>
+__device__ __forceinline__ void flat_result(const DModel& m, bool active, int w, int ln, Hit& h) {
+    FlatLds& L = flat_lds();
+    h.t = kMaxFloat;
+    h.face = 0;
+    h.u = h.v = 0.f;
+    const unsigned long long key = L.key[w][ln];
+    if (active && key != kKeyInit) {
+        h.t = __uint_as_float(uint32_t(key >> 32));
+        if constexpr (!NUV) {
+            h.u = L.u[w][ln];
+            h.v = L.v[w][ln];
+        }
+        h.face = __float_as_uint(m.prim[3 * size_t(L.slot[w][ln]) + 2].z);
+    }
+}
+
+// One tree query of every active lane of the wave (called by all 64 lanes, converged): passes and
+// leaf steps until every lane's query is done. Flags as above.
 template <bool COUNT, bool HYB = false, bool LDSB = false, bool UO = false, bool UT = false, bool NUV = false,
           bool NEAR = false>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
-    constexpr int K = kLeafBuf;
-    FlatLds& L = flat_lds();  // one instance per kernel, shared by every flavour of this scan
-    auto& s_lbd = L.lbd;
-    auto& s_lbl = L.lbl;
-    auto& s_key = L.key;
-    auto& s_slot = L.slot;
-    auto& s_u = L.u;
-    auto& s_v = L.v;
-    auto& s_mark = L.mark;
     const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
     ATR_PCLK(uint64_t tcs = clock64());
-    h.t = kMaxFloat;
-    h.face = 0;
-    h.u = h.v = 0.f;
-    // the re-walk bound (bd, bi) is the last leaf of the previous pass's full buffer (entry K - 1 of
-    // the LDS column), read when the pass starts; the ray's result stays in its LDS key/slot/u/v
-    // row once it is done (no register holds it through the scan)
-    bool done = true, need = false, more = false, rewalk = false;
-    int32_t j = 0, nb = 0;
-    s_key[w][ln] = kKeyInit;
-    if (active) {
-        const NodeBox root = load_node(m.nodes, 0);
-        if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
-        if (box_check(r, root.lx, root.ly, root.lz, root.hx, root.hy, root.hz)) {  // kd_tree.cpp:339
-            done = false;
-            if (root.children == 0) {  // :344-361: the root leaf (discovery rank 0) alone
-                s_lbl[w][0][ln] = 0;
-                s_lbd[w][0][ln] = 0.f;
-                nb = 1;
-            } else {
-                need = true;
-            }
-        }
-    }
+    FlatQ q = flat_begin<COUNT>(r, m, active, w, ln, ct);
     for (;;) {
         ATR_PCLK(const uint64_t tc0 = clock64());
-        const float bd = rewalk ? s_lbd[w][K - 1][ln] : -__builtin_inff();
-        const int32_t bi = rewalk ? s_lbl[w][K - 1][ln] : -1;
-        if constexpr (UT) {  // the wave walks its passes together (traverse_pass_wave)
-            if (__ballot(need)) {
-                LdsLeafBuf<K> lb;
-                lb.d = &s_lbd[w][0][ln];
-                lb.leaf = &s_lbl[w][0][ln];
-                const int32_t n = traverse_pass_wave<K, COUNT>(r, m.inner, lb, bd, bi, ct, need);
-                if (need) {
-                    need = false;
-                    j = 0;
-                    if (n < 0) { err = 1; done = true; }
-                    else { nb = n < K ? n : K; more = n > K; if (nb == 0) done = true; }
-                }
-            }
-        } else if (need) {  // one DFS pass (kd_tree.cpp:363-435); its sorted leaves wait in LDS
-            int32_t n;
-            if constexpr (LDSB) {
-                LdsLeafBuf<K> lb;
-                lb.d = &s_lbd[w][0][ln];
-                lb.leaf = &s_lbl[w][0][ln];
-                if (NEAR && m.near_ok) n = traverse_pass_near<K, COUNT>(r, m.inner, lb, bd, bi, ct);
-                else n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
-            } else {  // register buffer: the LDS one measured 5% slower for incoherent bounce rays
-                LeafBuf<K> lb;
-                n = traverse_pass<K, COUNT>(r, m.inner, lb, bd, bi, ct);
-#pragma unroll
-                for (int q = 0; q < K; ++q) { s_lbd[w][q][ln] = lb.d[q]; s_lbl[w][q][ln] = lb.leaf[q]; }
-            }
-            need = false;
-            j = 0;
-            if (n < 0) { err = 1; done = true; }
-            else { nb = n < K ? n : K; more = n > K; if (nb == 0) done = true; }
-        }
-        ATR_PCLK(const uint64_t tc2 = clock64());
-        ATR_PCLK(ct.t_pass += uint32_t(tc2 - tc0));
-        const uint64_t livem = __ballot(!done);
-        if (livem == 0) break;
-        // every live ray's current leaf: its clusters are this step's items
-        uint32_t cf = 0, cn = 0;
-        if (!done) {
-            const uint2_t cr = load_range(m.cl_range, s_lbl[w][j][ln]);
-            cf = cr.x;
-            cn = cr.y;
-            if constexpr (COUNT) { ct.leaf += 1; ct.cbox += cn; }
-        }
-        const uint32_t incl = wave_incl_add(cn);  // inclusive prefix sum over the lanes
-        const uint32_t excl = incl - cn;
-        const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
-        if (!done) s_key[w][ln] = kKeyInit;
-        bool deal = true;
-        if constexpr (HYB) {
-            // the largest cluster count of the step (counts are small: the signed max is exact)
-            const uint32_t mx = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
-            deal = int32_t(mx) > hyb_a * int32_t((total + 63u) >> 6) + hyb_b;
-        }
-        ATR_PCLK(const uint64_t tc1 = clock64());
-        ATR_PCLK(ct.t_prep += uint32_t(tc1 - tc2));
-        if (!deal) {  // every lane scans its own leaf's clusters, one per iteration; the candidates
-                      // of each iteration are compacted over the wave
-            const uint32_t mxc = uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cn)), 63));
-            for (uint32_t i = 0; i < mxc; ++i) {
-                uint32_t cm = 0;
-                if (i < cn) {
-                    const uint32_t c = cf + i;
-                    const float bound = __uint_as_float(uint32_t(s_key[w][ln] >> 32));
-                    cm = cluster_cands<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)],
-                                              m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
-                }
-                cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
-            }
-        }
-        ATR_PCLK(if (!deal) ct.t_lp += uint32_t(clock64() - tc1));
-        int32_t carry = -1;
-        for (uint32_t base = 0; deal && base < total; base += 64) {  // rounds of 64 items, wave-uniform
-            s_mark[w][ln] = -1;
-            __builtin_amdgcn_wave_barrier();
-            if (cn > 0 && excl >= base && excl < base + 64u) s_mark[w][excl - base] = ln;
-            __builtin_amdgcn_wave_barrier();
-            int32_t own = wave_incl_max(s_mark[w][ln]);  // latest owner starting at or before this lane
-            if (own < 0) own = carry;
-            carry = __builtin_amdgcn_readlane(own, 63);
-            const uint32_t k = base + uint32_t(ln);
-            const bool valid = k < total;
-            if constexpr (COUNT) { ct.round_wave += ln == 0 ? 1u : 0u; ct.round_items += valid ? 1u : 0u; }
-            const int32_t src = valid ? own : ln;
-            Ray q;  // the owner's ray
-            q.o = UO ? r.o : mk(shfl_f(r.o.x, src), shfl_f(r.o.y, src), shfl_f(r.o.z, src));
-            q.d = mk(shfl_f(r.d.x, src), shfl_f(r.d.y, src), shfl_f(r.d.z, src));
-            q.inv = mk(shfl_f(r.inv.x, src), shfl_f(r.inv.y, src), shfl_f(r.inv.z, src));
-            q.s0 = q.inv.x < 0;
-            q.s1 = q.inv.y < 0;
-            q.s2 = q.inv.z < 0;
-            const uint32_t c = uint32_t(__shfl(int(cf), src)) + (k - uint32_t(__shfl(int(excl), src)));
-            uint32_t cm = 0;
-            if (valid) {
-                const float bound = __uint_as_float(uint32_t(s_key[w][own] >> 32));
-                cm = cluster_cands<COUNT>(q, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1],
-                                          bound, ct);
-            }
-            cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
-        }
-        ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
-        if (!done) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
-            if (s_key[w][ln] != kKeyInit) {
-                done = true;
-            } else if (++j >= nb) {
-                if (more) need = rewalk = true;  // the next K leaves after this buffer's last
-                else done = true;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        flat_pass<COUNT, LDSB, UT, NEAR>(r, m, w, ln, q, err, ct);
+        ATR_PCLK(ct.t_pass += uint32_t(clock64() - tc0));
+        if (__ballot(!q.done) == 0) break;
+        flat_leaf_step<COUNT, HYB, UO, NUV>(r, m, w, ln, !q.done, q, ct, hyb_a, hyb_b);
     }
-    const unsigned long long key = s_key[w][ln];
-    if (active && key != kKeyInit) {
-        h.t = __uint_as_float(uint32_t(key >> 32));
-        if constexpr (!NUV) {
-            h.u = s_u[w][ln];
-            h.v = s_v[w][ln];
-        }
-        h.face = __float_as_uint(m.prim[3 * size_t(s_slot[w][ln]) + 2].z);
-    }
+    flat_result<NUV>(m, active, w, ln, h);
     ATR_PCLK(ct.t_scan += uint32_t(clock64() - tcs));
 }
 

@@ -9,7 +9,7 @@ for v in "$@"; do
   n=${v%%:*}
   d=${v#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 $F $d -shared -o ../_lib/exp/$n.so \
-    render.hip persist.hip wavefront.hip build.hip exchange.hip plan.hip capi.cpp host_scene.cpp obj_parse.cpp -lpthread &
+    render.hip paths.hip build.hip exchange.hip plan.hip capi.cpp host_scene.cpp obj_parse.cpp -lpthread &
 done
 wait
 ls -la ../_lib/exp/*.so
