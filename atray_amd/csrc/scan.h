@@ -171,20 +171,78 @@ __device__ __forceinline__ FlatLds& flat_lds() {
 
 constexpr unsigned long long kKeyInit = (static_cast<unsigned long long>(0x7F7FFFFFu) << 32) | 0xFFFFFFFFull;
 
-// Full tests of a round's candidates, compacted over the wavefront. Each lane holds one
-// (ray, cluster) item that passed the padded boxes and the screen with candidate mask `cm` (slots
-// cfirst + bit, ray of lane `own`); the wave's candidates are numbered by a prefix sum of the
-// masks' popcounts and dealt 64 per sub-round, one full test per lane. Each test lowers its owner's
-// (t bits, leaf rank) key in LDS -- the minimum over the leaf in any order is the reference's
-// first-in-leaf-order closest hit (kd_tree.cpp:440-456) -- and the winning test writes the slot
-// and barycentrics. UO: every ray of the wave has the same origin (camera rays).
-template <bool COUNT, bool UO, bool NUV>
+// One full test of candidate `slot` for the ray q of owner lane `ow`: lowers the owner's (t bits,
+// leaf rank) key in LDS -- the minimum over the leaf in any order is the reference's
+// first-in-leaf-order closest hit (kd_tree.cpp:440-456); true if this test lowered it.
+template <bool COUNT>
+__device__ __forceinline__ bool cand_test(const Ray& q, const DModel& m, int w, int32_t ow, uint32_t slot,
+                                          unsigned long long& mine, float& u, float& v, Ctr& ct) {
+    FlatLds& L = flat_lds();
+    if constexpr (COUNT) ct.tri += 1;
+    float4_t a0, a1, a2;
+    load_prim(m, slot, a0, a1, a2);
+    const float dist = tri_hit(q, mk(a0.x, a0.y, a0.z), mk(a0.w, a1.x, a1.y), mk(a1.z, a1.w, a2.x), u, v);
+    if (dist > kTol && dist < kMaxFloat) {  // accepted (model.h:75-103; kd_tree.cpp:450)
+        mine = (static_cast<unsigned long long>(__float_as_uint(dist)) << 32) | uint32_t(__float_as_int(a2.y));
+        if (mine < L.key[w][ow]) {
+            atomicMin(&L.key[w][ow], mine);
+            return true;
+        }
+    }
+    return false;
+}
+
+// Full tests of a step's candidates. Each lane holds one (ray, cluster) item that passed the padded
+// boxes and the screen with candidate mask `cm` (slots cfirst + bit, ray of lane `own`; SELF: every
+// lane's item is its own ray, the lane-private scan). Two schedules, chosen wave-uniformly (in place
+// only with SELF: in dealt steps it measured no use and its registers spilled), same result (the minimum key
+// does not depend on the order of the tests; the rank in the key makes keys unique within a leaf):
+//   in place -- when no lane holds more candidates than the compacted schedule would need
+//               sub-rounds, each lane tests its own candidates one per iteration (no numbering,
+//               owner lookup or ray shuffles per test);
+//   compacted -- the wave's candidates are numbered by a prefix sum of the masks' popcounts and
+//               dealt 64 per sub-round, one full test per lane.
+// The winning test of each (sub-)round writes its owner's slot and barycentrics. UO: every ray of
+// the wave has the same origin (camera rays).
+template <bool COUNT, bool UO, bool NUV, bool SELF = false>
 __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
                                             uint32_t cfirst, int32_t own, Ctr& ct) {
     FlatLds& L = flat_lds();
     const uint32_t cc = uint32_t(__popc(cm));
     const uint32_t cinc = wave_incl_add(cc);
     const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(cinc), 63));
+#ifdef ATR_NO_INPLACE
+    constexpr bool kInPlace = false;  // experiment build: compacted sub-rounds only
+#else
+    constexpr bool kInPlace = SELF;
+#endif
+    const uint32_t most = kInPlace ? uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cc)), 63)) : 64u;
+    if (kInPlace && most <= (total + 63u) >> 6) {  // in place: `most` iterations instead of as many sub-rounds
+        Ray q;
+        q.o = r.o;
+        q.d = r.d;
+        uint32_t x = cm;
+        for (uint32_t it = 0; it < most; ++it) {  // wave-uniform
+            const bool valid = x != 0;
+            const uint32_t slot = cfirst + (valid ? uint32_t(__builtin_ctz(x)) : 0u);
+            x &= x - 1u;
+            if constexpr (COUNT) ct.cand_wave += ln == 0 ? 1u : 0u;
+            unsigned long long mine = kKeyInit;
+            bool imp = false;
+            float u = 0.f, v = 0.f;
+            if (valid) imp = cand_test<COUNT>(q, m, w, own, slot, mine, u, v, ct);
+            __builtin_amdgcn_wave_barrier();
+            if (imp && L.key[w][own] == mine) {  // this iteration's winner for its owner
+                L.slot[w][own] = slot;
+                if constexpr (!NUV) {
+                    L.u[w][own] = u;
+                    L.v[w][own] = v;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        return;
+    }
     const uint32_t cex = cinc - cc;
     int32_t carry = -1;
     for (uint32_t cb = 0; cb < total; cb += 64) {  // wave-uniform
@@ -357,7 +415,7 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
                 cm = cluster_cands<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)],
                                           m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
             }
-            cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
+            cand_rounds<COUNT, UO, NUV, true>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
         }
     }
     ATR_PCLK(if (!deal) ct.t_lp += uint32_t(clock64() - tc1));
