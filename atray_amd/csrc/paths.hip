@@ -274,8 +274,10 @@ __global__ __launch_bounds__(256) void path_resolve_kernel(PathParams P) {
 }
 
 // Occupancy (waves/SIMD) of the two trace kernels, 5..7 (the LDS limit is 7: 22.5 KB per
-// workgroup); tuning path_camera_occ / path_bounce_occ pick another (0 = these defaults).
-constexpr int kCameraOcc = 7;
+// workgroup); tuning path_camera_occ / path_bounce_occ pick another (0 = these defaults). The
+// camera kernel at 7 spills 21 dwords whose write-backs reach HBM (14.9 GB per c4 frame against
+// 4.6 GB at 6) and is no faster.
+constexpr int kCameraOcc = 6;
 constexpr int kBounceOcc = 7;
 template __global__ void path_camera_kernel<false, 5>(PathParams);
 template __global__ void path_camera_kernel<false, 6>(PathParams);
