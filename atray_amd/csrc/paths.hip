@@ -191,17 +191,23 @@ __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
             o = mk(a.x, a.y, a.z);
             d = mk(a.w, b.x, b.y);
         }
-        Isect id;
-        id.type = T_NONE;
-        intersect_scene<SCHED_FLAT, FLAV_BOUNCE, COUNT>(S, o, d, valid, id, err, ct, P.hyb_a, P.hyb_b);
-        __asm__ volatile("" ::: "memory");  // the path state is read after the query, not held through it
+        const SceneHit sh = intersect_models<SCHED_FLAT, FLAV_BOUNCE, COUNT>(S, o, d, valid, err, ct, P.hyb_a, P.hyb_b);
+        // the path -- its ray too -- is read again after the query instead of being held through
+        // it: the memory clobber keeps the loads here, the opaque copy of the entry index keeps
+        // their addresses from being formed before the query
+        uint32_t ea = e;
+        __asm__ volatile("" : "+v"(ea) :: "memory");
         bool go = false;
         uint32_t pix = 0, g = 0;
         V3 ret = mk(0.f, 0.f, 0.f), w = mk(1.f, 1.f, 1.f);
         uint64_t st = 0;
         if (valid) {
             traced += 1;
-            const float4_t b = qin[P.cap + e], c = qin[2 * P.cap + e], q3 = qin[3 * P.cap + e];
+            const float4_t a = qin[ea], b = qin[P.cap + ea], c = qin[2 * P.cap + ea], q3 = qin[3 * P.cap + ea];
+            o = mk(a.x, a.y, a.z);
+            d = mk(a.w, b.x, b.y);
+            Isect id;
+            scene_finish(S, o, d, sh.best, sh.face, sh.fu, sh.fv, sh.nm, id);  // renderer.cpp:86-160
             pix = __float_as_uint(b.z);
             g = __float_as_uint(b.w);
             ret = mk(c.x, c.y, c.z);

@@ -525,17 +525,23 @@ __device__ __forceinline__ DModel uniform_model(const DModel& src) {
     return m;
 }
 
+// The models' closest triangle (renderer.cpp:34-82): best t, face, barycentrics, model (-1: none).
+struct SceneHit {
+    float best, fu, fv;
+    uint32_t face;
+    int32_t nm;
+};
+
 // get_intersection_data (renderer.cpp:34-160) for every lane of the wave (converged call; inactive
 // lanes take part in the wave-wide scans). SCHED_LANE: per-lane reference scan; otherwise the
-// clustered scan in flavour FLAV.
+// clustered scan in flavour FLAV. intersect_models is the models' part; scene_finish (shade.h) the
+// spheres, planes and hit record, so a caller can re-read o and d between the two instead of
+// holding them through the query.
 template <int SCHED, int FLAV, bool COUNT>
-__device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active, Isect& id,
-                                                int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
+__device__ __forceinline__ SceneHit intersect_models(const DScene* __restrict__ S, V3 o, V3 d, bool active, int& err,
+                                                    Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
-    float best = kMaxFloat;
-    int32_t nm = -1;
-    uint32_t face = 0;
-    float fu = 0.f, fv = 0.f;
+    SceneHit sh{kMaxFloat, 0.f, 0.f, 0u, -1};
     const int32_t nmodels = __builtin_amdgcn_readfirstlane(S->nmodels);  // uniform: an SGPR, not a VGPR
     for (int32_t i = 0; i < nmodels; ++i) {
         const DModel m = uniform_model(S->models[i]);
@@ -552,7 +558,7 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                 tree_closest_flat<COUNT, true, false, false, false, false>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else  // bounce rays: near-first passes into the LDS leaf buffer, every step dealt
                 tree_closest_flat<COUNT, false, true, false, false, false, true>(r, m, active, h, err, ct);
-            if (h.t > kTol && h.t < best) { best = h.t; face = h.face; fu = h.u; fv = h.v; nm = i; }
+            if (h.t > kTol && h.t < sh.best) { sh.best = h.t; sh.face = h.face; sh.fu = h.u; sh.fv = h.v; sh.nm = i; }
         } else if (active) {  // brute force (:58-82), face-ordered triangles, uniform loads
             if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
             if (box_entry(r, m.aabb[0], m.aabb[1], m.aabb[2], m.aabb[3], m.aabb[4], m.aabb[5]) != 0) {
@@ -562,13 +568,20 @@ __device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3
                     float u = 0.f, v = 0.f;
                     const float tt = tri_hit(r, mk(t->ax, t->ay, t->az), mk(t->abx, t->aby, t->abz),
                                              mk(t->acx, t->acy, t->acz), u, v);
-                    if (tt > kTol && tt < best) { best = tt; fu = u; fv = v; face = j; nm = i; }
+                    if (tt > kTol && tt < sh.best) { sh.best = tt; sh.fu = u; sh.fv = v; sh.face = j; sh.nm = i; }
                 }
             }
         }
     }
+    return sh;
+}
+
+template <int SCHED, int FLAV, bool COUNT>
+__device__ __forceinline__ void intersect_scene(const DScene* __restrict__ S, V3 o, V3 d, bool active, Isect& id,
+                                                int& err, Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
+    const SceneHit sh = intersect_models<SCHED, FLAV, COUNT>(S, o, d, active, err, ct, hyb_a, hyb_b);
     if (!active) return;
-    scene_finish(S, o, d, best, face, fu, fv, nm, id);  // :86-160
+    scene_finish(S, o, d, sh.best, sh.face, sh.fu, sh.fv, sh.nm, id);  // :86-160
 }
 
 // One non-sky bounce of cast_ray (renderer.cpp:231-258): the new ray and the path's colour and
