@@ -291,7 +291,8 @@ def main():
     ap.add_argument("--tuning", default="",
                     help="diagnostic: k=v,... scheduling knobs for atr_set_tuning (xcd_chunk, frame_rotate, hybrid_a, "
                          "hybrid_b, path_batch_log2, cluster_size, path_camera_occ, path_bounce_occ, primary_occ); outputs never change")
-    ap.add_argument("--side", type=int, default=64, help="shard tile side (pixels)")
+    ap.add_argument("--side", type=int, default=32,
+                    help="shard tile side (pixels); 32 balances the 8-way c3 plan ~4%% better than 64 (DESIGN.md §5)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
