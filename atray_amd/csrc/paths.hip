@@ -165,6 +165,10 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
 }
 
 // ------------------------------------------------------------------ bounce k of the queued paths
+// Leaf buffer entries of the bounce rays' queries (the scan is templated on it). 6 entries cut the
+// LDS to 18 KB per workgroup, enough for 8 waves/SIMD, but cost re-walks: c4 71.0 ms per frame at 7
+// waves and 72.1 at 8 (64 VGPRs, scratch in the hot loop) vs 69.5 with 8 entries.
+constexpr int kBounceLeafBuf = kLeafBuf;
 template <bool COUNT, int OCC>
 __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
     const int lane = threadIdx.x & 63;
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
             o = mk(a.x, a.y, a.z);
             d = mk(a.w, b.x, b.y);
         }
-        const SceneHit sh = intersect_models<SCHED_FLAT, FLAV_BOUNCE, COUNT>(S, o, d, valid, err, ct, P.hyb_a, P.hyb_b);
+        const SceneHit sh = intersect_models<SCHED_FLAT, FLAV_BOUNCE, COUNT, kBounceLeafBuf>(S, o, d, valid, err, ct, P.hyb_a, P.hyb_b);
         // the path -- its ray too -- is read again after the query instead of being held through
         // it: the memory clobber keeps the loads here, the opaque copy of the entry index keeps
         // their addresses from being formed before the query

@@ -156,16 +156,18 @@ __device__ __forceinline__ int32_t wave_incl_max(int32_t x) {
 
 // LDS of the FLAT/HYBRID scans (22.5 KB per 4-wave workgroup): the leaf order buffers (lane-private
 // columns), the per-owner best keys and hit records, the round's owner markers.
+template <int K = kLeafBuf>
 struct FlatLds {
-    float lbd[4][kLeafBuf][64];
-    int32_t lbl[4][kLeafBuf][64];
+    float lbd[4][K][64];
+    int32_t lbl[4][K][64];
     unsigned long long key[4][64];
     uint32_t slot[4][64];
     float u[4][64], v[4][64];
     int32_t mark[4][64];
 };
-__device__ __forceinline__ FlatLds& flat_lds() {
-    __shared__ FlatLds L;
+template <int K = kLeafBuf>
+__device__ __forceinline__ FlatLds<K>& flat_lds() {
+    __shared__ FlatLds<K> L;
     return L;
 }
 
@@ -174,10 +176,10 @@ constexpr unsigned long long kKeyInit = (static_cast<unsigned long long>(0x7F7FF
 // One full test of candidate `slot` for the ray q of owner lane `ow`: lowers the owner's (t bits,
 // leaf rank) key in LDS -- the minimum over the leaf in any order is the reference's
 // first-in-leaf-order closest hit (kd_tree.cpp:440-456); true if this test lowered it.
-template <bool COUNT>
+template <bool COUNT, int K = kLeafBuf>
 __device__ __forceinline__ bool cand_test(const Ray& q, const DModel& m, int w, int32_t ow, uint32_t slot,
                                           unsigned long long& mine, float& u, float& v, Ctr& ct) {
-    FlatLds& L = flat_lds();
+    FlatLds<K>& L = flat_lds<K>();
     if constexpr (COUNT) ct.tri += 1;
     float4_t a0, a1, a2;
     load_prim(m, slot, a0, a1, a2);
@@ -204,10 +206,10 @@ __device__ __forceinline__ bool cand_test(const Ray& q, const DModel& m, int w, 
 //               dealt 64 per sub-round, one full test per lane.
 // The winning test of each (sub-)round writes its owner's slot and barycentrics. UO: every ray of
 // the wave has the same origin (camera rays).
-template <bool COUNT, bool UO, bool NUV, bool SELF = false>
+template <bool COUNT, bool UO, bool NUV, bool SELF = false, int K = kLeafBuf>
 __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
                                             uint32_t cfirst, int32_t own, Ctr& ct) {
-    FlatLds& L = flat_lds();
+    FlatLds<K>& L = flat_lds<K>();
     const uint32_t cc = uint32_t(__popc(cm));
     const uint32_t cinc = wave_incl_add(cc);
     const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(cinc), 63));
@@ -230,7 +232,7 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
             unsigned long long mine = kKeyInit;
             bool imp = false;
             float u = 0.f, v = 0.f;
-            if (valid) imp = cand_test<COUNT>(q, m, w, own, slot, mine, u, v, ct);
+            if (valid) imp = cand_test<COUNT, K>(q, m, w, own, slot, mine, u, v, ct);
             __builtin_amdgcn_wave_barrier();
             if (imp && L.key[w][own] == mine) {  // this iteration's winner for its owner
                 L.slot[w][own] = slot;
@@ -309,9 +311,9 @@ struct FlatQ {
     bool done, need, more, rewalk;
 };
 
-template <bool COUNT>
+template <bool COUNT, int K = kLeafBuf>
 __device__ __forceinline__ FlatQ flat_begin(const Ray& r, const DModel& m, bool active, int w, int ln, Ctr& ct) {
-    FlatLds& L = flat_lds();
+    FlatLds<K>& L = flat_lds<K>();
     FlatQ q{0, 0, true, false, false, false};
     L.key[w][ln] = kKeyInit;
     if (active) {
@@ -334,10 +336,9 @@ __device__ __forceinline__ FlatQ flat_begin(const Ray& r, const DModel& m, bool 
 // One DFS pass (kd_tree.cpp:363-435) for every lane with `need`; its sorted leaves wait in LDS.
 // UT: the wave walks its passes together (traverse_pass_wave: coherent rays). LDSB: the pass inserts
 // straight into the LDS columns. NEAR (with LDSB): near-first passes (traverse_pass_near).
-template <bool COUNT, bool LDSB, bool UT, bool NEAR>
+template <bool COUNT, bool LDSB, bool UT, bool NEAR, int K = kLeafBuf>
 __device__ __forceinline__ void flat_pass(const Ray& r, const DModel& m, int w, int ln, FlatQ& q, int& err, Ctr& ct) {
-    constexpr int K = kLeafBuf;
-    FlatLds& L = flat_lds();
+    FlatLds<K>& L = flat_lds<K>();
     // the re-walk bound: the last leaf of the previous pass's full buffer (entry K - 1 of the column)
     const float bd = q.rewalk ? L.lbd[w][K - 1][ln] : -__builtin_inff();
     const int32_t bi = q.rewalk ? L.lbl[w][K - 1][ln] : -1;
@@ -380,10 +381,10 @@ __device__ __forceinline__ void flat_pass(const Ray& r, const DModel& m, int w, 
 // the visiting order (minimum (t, leaf rank)), so the choice changes no output bit. Then each live
 // lane stops at the first leaf that improved its hit (kd_tree.cpp:457-460), moves to its next
 // leaf, or asks for a re-walk. UO: one origin for the whole wave. NUV: u and v feed no output.
-template <bool COUNT, bool HYB, bool UO, bool NUV>
+template <bool COUNT, bool HYB, bool UO, bool NUV, int K = kLeafBuf>
 __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, int w, int ln, bool live, FlatQ& q,
                                                Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
-    FlatLds& L = flat_lds();
+    FlatLds<K>& L = flat_lds<K>();
     ATR_PCLK(const uint64_t tc2 = clock64());
     uint32_t cf = 0, cn = 0;
     if (live) {
@@ -415,7 +416,7 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
                 cm = cluster_cands<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)],
                                           m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
             }
-            cand_rounds<COUNT, UO, NUV, true>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
+            cand_rounds<COUNT, UO, NUV, true, K>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
         }
     }
     ATR_PCLK(if (!deal) ct.t_lp += uint32_t(clock64() - tc1));
@@ -446,7 +447,7 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
             cm = cluster_cands<COUNT>(qr, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1],
                                       bound, ct);
         }
-        cand_rounds<COUNT, UO, NUV>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
+        cand_rounds<COUNT, UO, NUV, false, K>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
     }
     ATR_PCLK(if (deal) ct.t_deal += uint32_t(clock64() - tc1));
     if (live) {  // stop at the first leaf that improved the hit (kd_tree.cpp:457-460)
@@ -461,9 +462,9 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
 }
 
 // The lane's result from its LDS row (t = kMaxFloat: no hit).
-template <bool NUV>
+template <bool NUV, int K = kLeafBuf>
 __device__ __forceinline__ void flat_result(const DModel& m, bool active, int w, int ln, Hit& h) {
-    FlatLds& L = flat_lds();
+    FlatLds<K>& L = flat_lds<K>();
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
@@ -481,20 +482,20 @@ __device__ __forceinline__ void flat_result(const DModel& m, bool active, int w,
 // One tree query of every active lane of the wave (called by all 64 lanes, converged): passes and
 // leaf steps until every lane's query is done. Flags as above.
 template <bool COUNT, bool HYB = false, bool LDSB = false, bool UO = false, bool UT = false, bool NUV = false,
-          bool NEAR = false>
+          bool NEAR = false, int K = kLeafBuf>
 __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m, bool active, Hit& h, int& err,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
     ATR_PCLK(uint64_t tcs = clock64());
-    FlatQ q = flat_begin<COUNT>(r, m, active, w, ln, ct);
+    FlatQ q = flat_begin<COUNT, K>(r, m, active, w, ln, ct);
     for (;;) {
         ATR_PCLK(const uint64_t tc0 = clock64());
-        flat_pass<COUNT, LDSB, UT, NEAR>(r, m, w, ln, q, err, ct);
+        flat_pass<COUNT, LDSB, UT, NEAR, K>(r, m, w, ln, q, err, ct);
         ATR_PCLK(ct.t_pass += uint32_t(clock64() - tc0));
         if (__ballot(!q.done) == 0) break;
-        flat_leaf_step<COUNT, HYB, UO, NUV>(r, m, w, ln, !q.done, q, ct, hyb_a, hyb_b);
+        flat_leaf_step<COUNT, HYB, UO, NUV, K>(r, m, w, ln, !q.done, q, ct, hyb_a, hyb_b);
     }
-    flat_result<NUV>(m, active, w, ln, h);
+    flat_result<NUV, K>(m, active, w, ln, h);
     ATR_PCLK(ct.t_scan += uint32_t(clock64() - tcs));
 }
 
@@ -537,7 +538,7 @@ struct SceneHit {
 // clustered scan in flavour FLAV. intersect_models is the models' part; scene_finish (shade.h) the
 // spheres, planes and hit record, so a caller can re-read o and d between the two instead of
 // holding them through the query.
-template <int SCHED, int FLAV, bool COUNT>
+template <int SCHED, int FLAV, bool COUNT, int KB = kLeafBuf>
 __device__ __forceinline__ SceneHit intersect_models(const DScene* __restrict__ S, V3 o, V3 d, bool active, int& err,
                                                     Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
     const Ray r = make_ray(o, d);  // renderer.cpp:41-44
@@ -557,7 +558,7 @@ __device__ __forceinline__ SceneHit intersect_models(const DScene* __restrict__ 
             else if constexpr (FLAV == FLAV_HYB_BOUNCE)
                 tree_closest_flat<COUNT, true, false, false, false, false>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else  // bounce rays: near-first passes into the LDS leaf buffer, every step dealt
-                tree_closest_flat<COUNT, false, true, false, false, false, true>(r, m, active, h, err, ct);
+                tree_closest_flat<COUNT, false, true, false, false, false, true, KB>(r, m, active, h, err, ct);
             if (h.t > kTol && h.t < sh.best) { sh.best = h.t; sh.face = h.face; sh.fu = h.u; sh.fv = h.v; sh.nm = i; }
         } else if (active) {  // brute force (:58-82), face-ordered triangles, uniform loads
             if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
