@@ -30,16 +30,6 @@ constexpr float kTau = 3e-3f;
 constexpr float kEps = 5.9604645e-8f;  // 2^-24
 constexpr float kPadRel = 36.0f * kEps, kPadAbs = 12.0f * kEps;
 
-// Best hit of one leaf scan in progress: t, primitive slot, barycentrics, leaf rank of the hit
-// taken in THIS leaf (-1: the best was carried in), whether this leaf improved it.
-struct LeafHit {
-    float t;
-    uint32_t slot;
-    float u, v;
-    int32_t rank;
-    bool improved;
-};
-
 // The full-test operands of slot k, one 48-B record {a.xyz, ab.x}{ab.yz, ac.xy}{ac.z, bits(leaf
 // rank), bits(face), 0}: one cache line (at most two) per test. (Round 3's three SoA streams
 // touched three lines per test; incoherent bounce rays miss in L2 on most of them)
