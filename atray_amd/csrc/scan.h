@@ -213,13 +213,15 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
     const uint32_t cc = uint32_t(__popc(cm));
     const uint32_t cinc = wave_incl_add(cc);
     const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(cinc), 63));
-#ifdef ATR_NO_INPLACE
-    constexpr bool kInPlace = false;  // experiment build: compacted sub-rounds only
-#else
     constexpr bool kInPlace = SELF;
-#endif
     const uint32_t most = kInPlace ? uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cc)), 63)) : 64u;
-    if (kInPlace && most <= (total + 63u) >> 6) {  // in place: `most` iterations instead of as many sub-rounds
+#ifndef ATR_INPLACE_FACTOR
+#define ATR_INPLACE_FACTOR 2
+#endif
+    // in place while every lane holds fewer than F x (compacted sub-rounds) candidates: an
+    // in-place iteration skips the numbering, owner lookup and shuffles of a sub-round (c3: in
+    // place up to 1 x the sub-rounds 7,618-7,735 Mrays/s, below 2 x 7,746-7,858)
+    if (kInPlace && most < ATR_INPLACE_FACTOR * ((total + 63u) >> 6)) {
         Ray q;
         q.o = r.o;
         q.d = r.d;
