@@ -211,17 +211,25 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
                                             uint32_t cfirst, int32_t own, Ctr& ct) {
     FlatLds<K>& L = flat_lds<K>();
     const uint32_t cc = uint32_t(__popc(cm));
-    const uint32_t cinc = wave_incl_add(cc);
-    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(cinc), 63));
     constexpr bool kInPlace = SELF;
-    const uint32_t most = kInPlace ? uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cc)), 63)) : 64u;
 #ifndef ATR_INPLACE_FACTOR
 #define ATR_INPLACE_FACTOR 2
 #endif
     // in place while every lane holds fewer than F x (compacted sub-rounds) candidates: an
     // in-place iteration skips the numbering, owner lookup and shuffles of a sub-round (c3: in
     // place up to 1 x the sub-rounds 7,618-7,735 Mrays/s, below 2 x 7,746-7,858)
-    if (kInPlace && most < ATR_INPLACE_FACTOR * ((total + 63u) >> 6)) {
+    uint32_t cinc = 0, total = 0, most;
+    bool inplace;
+    if (kInPlace && __ballot(cc > 1u) == 0) {  // at most one candidate per lane: in place, no scans
+        most = __ballot(cc != 0u) ? 1u : 0u;    // (c3 +2%)
+        inplace = true;
+    } else {
+        cinc = wave_incl_add(cc);
+        total = uint32_t(__builtin_amdgcn_readlane(int(cinc), 63));
+        most = kInPlace ? uint32_t(__builtin_amdgcn_readlane(wave_incl_max(int32_t(cc)), 63)) : 64u;
+        inplace = kInPlace && most < ATR_INPLACE_FACTOR * ((total + 63u) >> 6);
+    }
+    if (inplace) {
         Ray q;
         q.o = r.o;
         q.d = r.d;
