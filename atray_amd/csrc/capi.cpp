@@ -1069,7 +1069,7 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                 std::vector<float4_t> pr(3 * ns, float4_t{0.f, 0.f, 0.f, 0.f});
                 // screen normals, 24 u32 per cluster: (nx, ny) of slot k as f16 in word k, then
                 // (nz of slot 2i, nz of slot 2i + 1) in word 16 + i (cluster.h)
-                std::vector<uint32_t> nw(std::max<size_t>(1, ncl) * 24, 0u);
+                std::vector<uint32_t> nw(std::max<size_t>(1, ncl) * kNormWords, 0u);
                 for (size_t cl = 0; cl < ncl; ++cl) {
                     uint32_t pw, first;
                     std::memcpy(&pw, &C.rec[8 * cl + 3], 4);
@@ -1100,15 +1100,15 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
                             v = std::max(-511L, std::min(511L, v));
                             h[a] = half_of_int(int32_t(v));
                         }
-                        nw[24 * cl + i] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
-                        nw[24 * cl + 16 + i / 2] |= uint32_t(h[2]) << (16 * (i & 1));
+                        nw[kNormWords * cl + i] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
+                        nw[kNormWords * cl + kMaxClusterSize + i / 2] |= uint32_t(h[2]) << (16 * (i & 1));
                     }
                 }
                 // one 128-B block per cluster: record {lo, P}{hi, q}, then its 24 normal words
                 std::vector<uint32_t> blk(std::max<size_t>(1, ncl) * 4 * kClusterBlock, 0u);
                 for (size_t cl = 0; cl < ncl; ++cl) {
                     std::memcpy(&blk[4 * kClusterBlock * cl], &C.rec[8 * cl], 8 * sizeof(float));
-                    std::memcpy(&blk[4 * kClusterBlock * cl + 8], &nw[24 * cl], 24 * sizeof(uint32_t));
+                    std::memcpy(&blk[4 * kClusterBlock * cl + 8], &nw[kNormWords * cl], kNormWords * sizeof(uint32_t));
                 }
                 if ((rc = dev_upload(c, blk.data(), blk.size() * sizeof(uint32_t), &p))) return rc;
                 dm.clus = static_cast<const float4_t*>(p);

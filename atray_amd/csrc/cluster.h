@@ -153,7 +153,7 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
     const float blo = b - fabsf(b) * 9.5367432e-7f - 1.1754944e-38f;
     uint32_t cand = 0;
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
-        cand |= screen8(sr, blo, ahi, nb[g / 4], nb[g / 4 + 1], nb[4 + g / 8]) << g;
+        cand |= screen8(sr, blo, ahi, nb[g / 4], nb[g / 4 + 1], nb[kMaxClusterSize / 4 + g / 8]) << g;
     return cand & slots;
 }
 

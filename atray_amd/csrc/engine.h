@@ -29,9 +29,12 @@ constexpr int kMaskLevels = 16;                   // traversal mask-stack depth 
 constexpr int kMaxMaterials = 32;
 constexpr int kMaxFrameCams = 16;  // distinct cameras per multi-frame launch (kernel argument)
 constexpr int kMaxModels = 8;
-constexpr int kMaxClusterSize = 16;  // primitive slots per leaf cluster (ATR_CLUSTER_SIZE <= this)
-constexpr int kClusterBlock = 8;     // 16-B words per cluster block (one 128-B line): record (2),
-                                     // screen normals (6)
+// Primitive slots per leaf cluster (atr_tuning.cluster_size <= this) and 16-B words per cluster
+// block (one 128-B line: record (2), screen normals (6)). 32 slots in 256-B blocks measured slower
+// (DESIGN.md §4b); the layout code is written for either.
+constexpr int kMaxClusterSize = 16;
+constexpr int kClusterBlock = 8;
+constexpr int kNormWords = kMaxClusterSize + kMaxClusterSize / 2;  // u32 screen-normal words per cluster
 
 struct V3 { float x, y, z; };
 ATR_HD V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }

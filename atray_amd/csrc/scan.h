@@ -271,6 +271,9 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
         uint32_t j = k - uint32_t(__shfl(int(cex), s2));
         uint32_t x = uint32_t(__shfl(int(cm), s2));
         uint32_t b = 0, n;  // position of the j-th set bit of the 16-bit mask x
+        if constexpr (kMaxClusterSize > 16) {
+            n = uint32_t(__popc(x & 0xFFFFu)); if (j >= n) { j -= n; x >>= 16; b += 16; }
+        }
         n = uint32_t(__popc(x & 0xFFu)); if (j >= n) { j -= n; x >>= 8; b += 8; }
         n = uint32_t(__popc(x & 0xFu)); if (j >= n) { j -= n; x >>= 4; b += 4; }
         n = uint32_t(__popc(x & 0x3u)); if (j >= n) { j -= n; x >>= 2; b += 2; }
