@@ -873,7 +873,7 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
     if (!c || !t) return ATR_E_INVALID;
     if (t->xcd_chunk < 0 || t->xcd_chunk > 4096 || t->frame_rotate < 0 || t->frame_rotate > 1024 ||
         t->hybrid_a < -4096 || t->hybrid_a > 4096 || t->hybrid_b < -4096 || t->hybrid_b > 4096 ||
-        t->path_batch_log2 < 12 || t->path_batch_log2 > 30 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
+        t->path_batch_log2 < 12 || t->path_batch_log2 > 28 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
         t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
         (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)) ||
         (t->primary_occ != 0 && t->primary_occ != 6 && t->primary_occ != 7))

@@ -308,6 +308,8 @@ def test_tuning_changes_no_output(eng, variant):
         eng.set_tuning(cluster_size=17)
     with pytest.raises(E.AtrError):
         eng.set_tuning(xcd_chunk=-1)
+    with pytest.raises(E.AtrError):
+        eng.set_tuning(path_batch_log2=29)
     assert eng.tuning() == base
 
 
