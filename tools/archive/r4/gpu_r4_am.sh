@@ -1,7 +1,7 @@
 #!/bin/bash
 # c4: path batch size (atr_tuning.path_batch_log2) -- 2^27 paths (one c4 frame, default) vs
 # smaller batches whose queues (144 B per path) fit the 256 MB MALL: 2^25, 2^23, 2^21, 2^20;
-# `bash tools/gpu_r4_am.sh big`: 2^28 and 2^29 (2 and 4 c4 frames per batch).
+# `bash tools/archive/r4/gpu_r4_am.sh big`: 2^28 and 2^29 (2 and 4 c4 frames per batch).
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4am
