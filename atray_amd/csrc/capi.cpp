@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <fcntl.h>
 #include <unistd.h>
 #include <cerrno>
@@ -175,15 +176,6 @@ void build_blocks(const atr_tile* tiles, int32_t ntiles, int32_t W, int32_t H, s
     for (size_t i = 0; i < out.size(); ++i) out[i].base = int32_t(i);
 }
 
-// IEEE binary16 bits of an integer |v| <= 2047 (exact).
-uint16_t half_of_int(int32_t v) {
-    if (v == 0) return 0;
-    const uint32_t sign = v < 0 ? 0x8000u : 0u;
-    uint32_t m = uint32_t(v < 0 ? -v : v);
-    int e = 31 - __builtin_clz(m);
-    return uint16_t(sign | (uint32_t(e + 15) << 10) | ((m << (10 - e)) & 0x3FFu));
-}
-
 // load_model_data's pool size (OBJ_loader.cpp:298: one chunk per pool thread): the host's
 // hardware threads, at most 16.
 int32_t default_parse_threads() {
@@ -240,7 +232,11 @@ struct atr_ctx {
         DevBuf mem;
         int64_t cap = 0;
         int32_t levels = 0;
+        hipEvent_t ev = nullptr;  // recorded after the latest launch that used `mem`
+        uint64_t last_use = 0;
     };
+    static constexpr size_t kMaxPathWS = 4;  // workspaces at most (streams beyond share them)
+    uint64_t ws_clock = 0;
     std::vector<PathWS> path_ws;
     // launches' traced-ray counter sets: a ring, each set reused only after the launch that last
     // used it (event) has finished; zeroed by its finish kernel
@@ -406,7 +402,10 @@ int sched_of(int32_t variant) {
 // dealt rounds for the stragglers); everything else on the sample-parallel path engine (a pixel's
 // samples side by side, one launch per bounce), or the FLAT cell megakernel for paths deeper than
 // its bounce launches.
+// -1: not a variant of this build, or a request it cannot run (PATHS beyond its bounce launches):
+// every entry point answers ATR_E_INVALID before it changes any state.
 int auto_sched(int32_t variant, const atr_camera& cam) {
+    if (variant == ATR_KERNEL_PATHS && cam.bounce_limit > kMaxPathBounces) return -1;
     if (variant != ATR_KERNEL_AUTO) return sched_of(variant);
     if (cam.bounce_limit == 1 && !cam.anti_aliasing && cam.samples_per_pixel == 1) return sched_of(ATR_KERNEL_HYBRID);
     return cam.bounce_limit <= kMaxPathBounces ? kSchedPaths : sched_of(ATR_KERNEL_FLAT);
@@ -475,27 +474,64 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
 }
 
 // The path engine's workspace for stream s, at least `cap` paths per batch and `levels` bounce
-// levels. Growing waits for every launch of the context (the old buffers may still be read).
+// levels. Each workspace belongs to the stream that used it last; a stream without one takes over
+// an idle workspace (its last launch finished), else opens a new one while there are fewer than
+// kMaxPathWS, else takes the least recently used one after a GPU-side wait on that workspace's last
+// launch. So the total stays bounded however many streams render. Growing a workspace waits for
+// its own last launch only. When the device has no memory for it, idle workspaces of other streams
+// are released and the allocation retried once; hipErrorOutOfMemory then goes back to the caller
+// (launch_paths halves its batch, launch_kernels falls back to FLAT).
 hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, atr_ctx::PathWS*& out) {
     atr_ctx::PathWS* ws = nullptr;
+    hipError_t e;
     for (auto& w : c->path_ws)
         if (w.stream == s) ws = &w;
-    if (!ws) {
+    if (!ws)
+        for (auto& w : c->path_ws)
+            if (!ws && w.ev && hipEventQuery(w.ev) == hipSuccess) ws = &w;
+    if (!ws && c->path_ws.size() < atr_ctx::kMaxPathWS) {
         c->path_ws.emplace_back();
         ws = &c->path_ws.back();
-        ws->stream = s;
+        if ((e = hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming)) != hipSuccess) return e;
     }
+    if (!ws) {
+        ws = &c->path_ws[0];
+        for (auto& w : c->path_ws)
+            if (w.last_use < ws->last_use) ws = &w;
+    }
+    if (ws->stream != s && ws->mem.p && (e = hipStreamWaitEvent(s, ws->ev, 0)) != hipSuccess) return e;
+    ws->stream = s;
+    ws->last_use = ++c->ws_clock;
     if (ws->cap < cap || ws->levels < levels) {
-        hipError_t e;
-        if ((e = wait_all(c)) != hipSuccess) return e;
+        if ((e = hipEventSynchronize(ws->ev)) != hipSuccess) return e;
         if (ws->mem.p && (e = hipFree(ws->mem.p)) != hipSuccess) return e;
         ws->mem = DevBuf();
-        ws->cap = std::max(ws->cap, cap);
-        ws->levels = std::max(ws->levels, levels);
+        const int64_t ncap = std::max(ws->cap, cap);
+        const int32_t nlev = std::max(ws->levels, levels);
+        ws->cap = 0;
+        ws->levels = 0;
         // 2 queues x kPathPlanes planes + the per-path results, 16 B per entry; the level counters
-        const size_t bytes = size_t(ws->cap) * 16 * (2 * kPathPlanes + 1) + size_t(ws->levels) * sizeof(PathCtl);
-        if ((e = hipMalloc(&ws->mem.p, bytes)) != hipSuccess) { ws->cap = 0; ws->levels = 0; return e; }
+        const size_t bytes = size_t(ncap) * 16 * (2 * kPathPlanes + 1) + size_t(nlev) * sizeof(PathCtl);
+        e = hipMalloc(&ws->mem.p, bytes);
+        if (e == hipErrorOutOfMemory) {
+            (void)hipGetLastError();
+            for (auto& w : c->path_ws)
+                if (&w != ws && w.mem.p && hipEventQuery(w.ev) == hipSuccess) {
+                    (void)hipFree(w.mem.p);
+                    w.mem = DevBuf();
+                    w.cap = 0;
+                    w.levels = 0;
+                }
+            e = hipMalloc(&ws->mem.p, bytes);
+        }
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            ws->mem = DevBuf();
+            return e;
+        }
         ws->mem.n = bytes;
+        ws->cap = ncap;
+        ws->levels = nlev;
     }
     out = ws;
     return hipSuccess;
@@ -510,18 +546,24 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     if (P.nblocks <= 0) return hipSuccess;
     if (bl > kMaxPathBounces) return hipErrorInvalidValue;
     const int64_t per_cell = 64 * std::max<int64_t>(spp, 1);
-    const int64_t batch = std::max<int64_t>(1, (int64_t(1) << c->tune.path_batch_log2) / per_cell);
-    const int64_t cells = std::min<int64_t>(batch, P.nblocks);
     const int32_t levels = std::max(bl, 1);
-    // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
-    // one-frame launch already holds the batch of the multi-frame launches that follow it (a
-    // regrowth waits for every stream of the context)
-    int64_t cap = 1;
-    while (cap < cells * per_cell) cap <<= 1;
-    cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
     atr_ctx::PathWS* ws = nullptr;
-    hipError_t e;
-    if ((e = path_workspace(c, s, cap, std::max(levels, 8), ws)) != hipSuccess) return e;
+    hipError_t e = hipErrorOutOfMemory;
+    int64_t cells = 0;
+    // a batch of 2^path_batch_log2 paths, halved while the device cannot hold its workspace (down to
+    // 2^16 paths; the outputs do not depend on the batch size)
+    for (int32_t lg = c->tune.path_batch_log2; lg >= 16 && e == hipErrorOutOfMemory; --lg) {
+        const int64_t batch = std::max<int64_t>(1, (int64_t(1) << lg) / per_cell);
+        cells = std::min<int64_t>(batch, P.nblocks);
+        // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
+        // one-frame launch already holds the batch of the multi-frame launches that follow it
+        int64_t cap = 1;
+        while (cap < cells * per_cell) cap <<= 1;
+        cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
+        e = path_workspace(c, s, cap, std::max(levels, 8), ws);
+        if (e == hipSuccess && ws->cap < cap) e = hipErrorOutOfMemory;
+    }
+    if (e != hipSuccess) return e;
     PathParams Q;
     std::memset(&Q, 0, sizeof(Q));
     Q.cam = P.cam;
@@ -566,11 +608,15 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
         }
         if ((e = atr_launch_path_resolve(Q, s)) != hipSuccess) return e;
     }
-    return hipSuccess;
+    return hipEventRecord(ws->ev, s);
 }
 
 hipError_t launch_kernels(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
-    if (sched == kSchedPaths) return launch_paths(c, P, s);
+    if (sched == kSchedPaths) {
+        const hipError_t e = launch_paths(c, P, s);
+        if (e != hipErrorOutOfMemory) return e;
+        sched = sched_of(ATR_KERNEL_FLAT);  // no memory for a path workspace: the cell megakernel,
+    }                                        // which needs none (same outputs)
     return atr_launch_render(P, sched, c->tune.primary_occ, s);
 }
 
@@ -904,8 +950,10 @@ int atr_destroy(atr_ctx* c) {
         for (auto& se : b.evs) (void)hipEventDestroy(se.second);
     }
     for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
-    for (auto& w : c->path_ws)
+    for (auto& w : c->path_ws) {
         if (w.mem.p) (void)hipFree(w.mem.p);
+        if (w.ev) (void)hipEventDestroy(w.ev);
+    }
     if (c->d_error) (void)hipFree(c->d_error);
     for (DevBuf& b : c->prog_blocks)
         if (b.p) (void)hipFree(b.p);
@@ -966,17 +1014,6 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
         dm.material = md.material;
         std::memcpy(dm.aabb, md.surrounding_aabb, sizeof(dm.aabb));
         dm.smooth = M.normals.empty() ? 0 : 1;
-        auto make_tri = [](const float* v, uint32_t face) {
-            DTri t;
-            std::memset(&t, 0, sizeof(t));
-            const V3 a = mk(v[0], v[1], v[2]), b = mk(v[3], v[4], v[5]), cc = mk(v[6], v[7], v[8]);
-            const V3 ab = sub(b, a), ac = sub(cc, a);  // model.h:77-78, once per primitive
-            t.ax = a.x; t.ay = a.y; t.az = a.z;
-            t.abx = ab.x; t.aby = ab.y; t.abz = ab.z;
-            t.acx = ac.x; t.acy = ac.y; t.acz = ac.z;
-            t.face = face;
-            return t;
-        };
         // per-face shading record (renderer.cpp:124-149)
         std::vector<float> shade(9 * (nf ? nf : 1), 0.f);
         for (size_t f = 0; f < nf; ++f) {
@@ -1000,139 +1037,32 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
         dm.shade = static_cast<const float*>(p);
         if (md.tree) {
             const HostTree& T = md.tree->t;
-            std::vector<DNode> nodes(size_t(T.nnodes));
-            std::vector<uint32_t> range(2 * size_t(T.nnodes), 0);
-            for (int32_t n = 0; n < T.nnodes; ++n) {
-                DNode& d = nodes[size_t(n)];
-                const float* b = &T.bounds[6 * size_t(n)];
-                d.lo_x = b[0]; d.lo_y = b[1]; d.lo_z = b[2];
-                d.hi_x = b[3]; d.hi_y = b[4]; d.hi_z = b[5];
-                d.children = T.children[size_t(n)];
-                d.parent = T.parent[size_t(n)];
-                range[2 * size_t(n)] = T.leaf_first[size_t(n)];
-                range[2 * size_t(n) + 1] = T.children[size_t(n)] ? 0u : T.leaf_count[size_t(n)];
-                if (T.depth[size_t(n)] > c->max_depth) c->max_depth = T.depth[size_t(n)];
-            }
-            // leaves are addressed by their static discovery rank on the device (inner_table)
-            std::vector<int32_t> leaf_rank;
-            {
-                std::vector<float4_t> inner;
-                if ((rc = inner_table(T, inner, leaf_rank))) return rc;
-                dm.ninner = int32_t(inner.size() / 3);
-                if (inner.empty()) inner.assign(3, float4_t{0.f, 0.f, 0.f, 0.f});
-                if ((rc = dev_upload(c, inner.data(), inner.size() * sizeof(float4_t), &p))) return rc;
-                dm.inner = static_cast<const float4_t*>(p);
-                if (dm.ninner > c->max_inner) c->max_inner = dm.ninner;
-            }
-            auto by_rank = [&](const std::vector<uint32_t>& per_node) {
-                std::vector<uint32_t> out(std::max<size_t>(2, per_node.size()), 0u);
-                for (int32_t n = 0; n < T.nnodes; ++n) {
-                    const int32_t k = leaf_rank[size_t(n)];
-                    if (k < 0) continue;
-                    out[2 * size_t(k)] = per_node[2 * size_t(n)];
-                    out[2 * size_t(k) + 1] = per_node[2 * size_t(n) + 1];
-                }
-                return out;
+            PackedTree PT;  // every device table of the model (host_scene.cpp pack_tree)
+            if ((rc = pack_tree(T, c->tune.cluster_size, PT))) return rc;
+            c->max_depth = std::max(c->max_depth, PT.max_depth);
+            auto up = [&](const auto& v, auto*& dst) {
+                void* q = nullptr;
+                const int r = dev_upload(c, v.data(), v.size() * sizeof(v[0]), &q);
+                dst = static_cast<std::remove_reference_t<decltype(dst)>>(q);
+                return r;
             };
-            range = by_rank(range);
-            std::vector<DTri> tris(T.prim_face.size());
-            for (size_t k = 0; k < tris.size(); ++k) tris[k] = make_tri(&T.prim_vertices[9 * k], T.prim_face[k]);
-            {
-                const size_t np = tris.size() ? tris.size() : 1;
-                std::vector<float4_t> s0(np), s1(np);
-                std::vector<float> s2(np, 0.f);
-                std::vector<uint32_t> sf(np, 0u);
-                for (size_t k = 0; k < tris.size(); ++k) {
-                    const DTri& t = tris[k];
-                    s0[k] = float4_t{t.ax, t.ay, t.az, t.abx};
-                    s1[k] = float4_t{t.aby, t.abz, t.acx, t.acy};
-                    s2[k] = t.acz;
-                    sf[k] = t.face;
-                }
-                if ((rc = dev_upload(c, s0.data(), s0.size() * sizeof(float4_t), &p))) return rc;
-                dm.t0 = static_cast<const float4_t*>(p);
-                if ((rc = dev_upload(c, s1.data(), s1.size() * sizeof(float4_t), &p))) return rc;
-                dm.t1 = static_cast<const float4_t*>(p);
-                if ((rc = dev_upload(c, s2.data(), s2.size() * sizeof(float), &p))) return rc;
-                dm.t2 = static_cast<const float*>(p);
-                if ((rc = dev_upload(c, sf.data(), sf.size() * sizeof(uint32_t), &p))) return rc;
-                dm.tface = static_cast<const uint32_t*>(p);
-            }
-            {  // clustered copy of the leaf primitives
-                LeafClusters C;
-                if ((rc = leaf_clusters(T, c->tune.cluster_size, C))) return rc;
-                // every cluster owns kMaxClusterSize consecutive slots (its first slot is 16 c), so
-                // the record's last word can carry the screen normals' step instead
-                const size_t ncl = C.rec.size() / 8;
-                const size_t ns = std::max<size_t>(1, ncl) * kMaxClusterSize;
-                // full-test records, 48 B per slot (cluster.h load_prim)
-                std::vector<float4_t> pr(3 * ns, float4_t{0.f, 0.f, 0.f, 0.f});
-                // screen normals, 24 u32 per cluster: (nx, ny) of slot k as f16 in word k, then
-                // (nz of slot 2i, nz of slot 2i + 1) in word 16 + i (cluster.h)
-                std::vector<uint32_t> nw(std::max<size_t>(1, ncl) * kNormWords, 0u);
-                for (size_t cl = 0; cl < ncl; ++cl) {
-                    uint32_t pw, first;
-                    std::memcpy(&pw, &C.rec[8 * cl + 3], 4);
-                    std::memcpy(&first, &C.rec[8 * cl + 7], 4);
-                    const uint32_t n = (pw & 31u) + 1u;
-                    if (n > uint32_t(kMaxClusterSize)) return ATR_E_INVALID;
-                    // screen normals: a step q >= max |n component| / 511 and each normal as
-                    // round(n / q), integers of at most 511 (exact in f16; |n - q p| <= q / 2)
-                    double mx = 0.0;
-                    for (uint32_t k = first; k < first + n; ++k)
-                        for (int a = 0; a < 3; ++a) mx = std::max(mx, std::fabs(double(C.normal[3 * k + a])));
-                    float q = float(mx / 511.0);
-                    while (double(q) * 511.0 < mx) q = std::nextafter(q, INFINITY);
-                    if (!(q > 0.f)) q = 1e-30f;
-                    C.rec[8 * cl + 7] = q;
-                    for (uint32_t i = 0; i < n; ++i) {
-                        const size_t k = first + i, slot = cl * kMaxClusterSize + i;
-                        const DTri& t = tris[C.order[k]];
-                        float rk, fc;
-                        std::memcpy(&rk, &C.rank[k], 4);
-                        std::memcpy(&fc, &t.face, 4);
-                        pr[3 * slot] = float4_t{t.ax, t.ay, t.az, t.abx};
-                        pr[3 * slot + 1] = float4_t{t.aby, t.abz, t.acx, t.acy};
-                        pr[3 * slot + 2] = float4_t{t.acz, rk, fc, 0.f};
-                        uint16_t h[3];
-                        for (int a = 0; a < 3; ++a) {
-                            long v = std::lround(double(C.normal[3 * k + a]) / double(q));
-                            v = std::max(-511L, std::min(511L, v));
-                            h[a] = half_of_int(int32_t(v));
-                        }
-                        nw[kNormWords * cl + i] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
-                        nw[kNormWords * cl + kMaxClusterSize + i / 2] |= uint32_t(h[2]) << (16 * (i & 1));
-                    }
-                }
-                // one 128-B block per cluster: record {lo, P}{hi, q}, then its 24 normal words
-                std::vector<uint32_t> blk(std::max<size_t>(1, ncl) * 4 * kClusterBlock, 0u);
-                for (size_t cl = 0; cl < ncl; ++cl) {
-                    std::memcpy(&blk[4 * kClusterBlock * cl], &C.rec[8 * cl], 8 * sizeof(float));
-                    std::memcpy(&blk[4 * kClusterBlock * cl + 8], &nw[kNormWords * cl], kNormWords * sizeof(uint32_t));
-                }
-                if ((rc = dev_upload(c, blk.data(), blk.size() * sizeof(uint32_t), &p))) return rc;
-                dm.clus = static_cast<const float4_t*>(p);
-                dm.cnrm = reinterpret_cast<const uint4_t*>(dm.clus + 2);
-                C.range = by_rank(C.range);
-                if ((rc = dev_upload(c, C.range.data(), C.range.size() * sizeof(uint32_t), &p))) return rc;
-                dm.cl_range = static_cast<const uint32_t*>(p);
-                if ((rc = dev_upload(c, pr.data(), pr.size() * sizeof(float4_t), &p))) return rc;
-                dm.prim = static_cast<const float4_t*>(p);
-                c->nclusters += int64_t(ncl);
-            }
-            if ((rc = dev_upload(c, nodes.data(), nodes.size() * sizeof(DNode), &p))) return rc;
-            dm.nodes = static_cast<const DNode*>(p);
-            if ((rc = dev_upload(c, range.data(), range.size() * sizeof(uint32_t), &p))) return rc;
-            dm.leaf_range = static_cast<const uint32_t*>(p);
-            if ((rc = dev_upload(c, tris.data(), tris.size() * sizeof(DTri), &p))) return rc;
-            dm.tris = static_cast<const DTri*>(p);
+            dm.ninner = PT.ninner;
+            if (dm.ninner > c->max_inner) c->max_inner = dm.ninner;
+            if ((rc = up(PT.inner, dm.inner)) || (rc = up(PT.t0, dm.t0)) || (rc = up(PT.t1, dm.t1)) ||
+                (rc = up(PT.t2, dm.t2)) || (rc = up(PT.tface, dm.tface)))
+                return rc;
+            const float4_t* clus = nullptr;
+            if ((rc = up(PT.clus, clus))) return rc;
+            dm.clus = clus;
+            dm.cnrm = reinterpret_cast<const uint4_t*>(dm.clus + 2);
+            if ((rc = up(PT.cl_range, dm.cl_range)) || (rc = up(PT.prim, dm.prim))) return rc;
+            c->nclusters += int64_t(PT.nclusters);
+            if ((rc = up(PT.nodes, dm.nodes)) || (rc = up(PT.leaf_range, dm.leaf_range))) return rc;
+            if (PT.tris.empty()) PT.tris.resize(1);
+            if ((rc = up(PT.tris, dm.tris))) return rc;
             dm.has_tree = 1;
             dm.root_leaf = T.children[0] == 0;
-            {
-                int32_t depth = 0;
-                for (int32_t d : T.depth) depth = std::max(depth, d);
-                dm.near_ok = depth <= 8 && dm.ninner < 65536;  // traverse_pass_near's register stack
-            }
+            dm.near_ok = PT.near_ok;
             if (T.nnodes > c->max_nodes) c->max_nodes = T.nnodes;
         } else {  // brute force: face-ordered triangles straight from the mesh (renderer.cpp:61-66)
             std::vector<DTri> tris(nf);
@@ -1183,6 +1113,17 @@ int atr_scene_info(atr_ctx* c, int64_t* bytes, int32_t* max_nodes, int32_t* max_
     return ATR_OK;
 }
 
+int atr_workspace_info(atr_ctx* c, int32_t* workspaces, int64_t* bytes) {
+    if (!c) return ATR_E_INVALID;
+    int32_t n = 0;
+    int64_t b = 0;
+    for (const auto& w : c->path_ws)
+        if (w.mem.p) { ++n; b += int64_t(w.mem.n); }
+    if (workspaces) *workspaces = n;
+    if (bytes) *bytes = b;
+    return ATR_OK;
+}
+
 int64_t atr_render_packed_size(const atr_tile* tiles, int32_t ntiles) {
     if (!tiles || ntiles <= 0) return 0;
     int32_t W = 0, H = 0;
@@ -1223,13 +1164,13 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     if (fr->layout != ATR_LAYOUT_IMAGE && fr->layout != ATR_LAYOUT_PACKED) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
+    const int wave = auto_sched(variant, *cam);
+    if (wave < 0) return ATR_E_INVALID;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
     int rc = ATR_OK;
     BlockSet* bs = get_blocks(c, tiles, ntiles, cam->width, cam->height, rc);
     if (!bs) return rc;
     c->prog_active = false;
-    const int wave = auto_sched(variant, *cam);
-    if (wave < 0) return ATR_E_INVALID;
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.cam = *cam;
@@ -1523,6 +1464,8 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
         return ATR_E_INVALID;
     if (cam->width <= 0 || cam->height <= 0 || cam->width > (1 << 16) || cam->height > (1 << 16)) return ATR_E_INVALID;
     if (fr->layout != ATR_LAYOUT_IMAGE) return ATR_E_INVALID;
+    const int sched = auto_sched(variant, *cam);
+    if (sched < 0) return ATR_E_INVALID;
     if (!c->d_scene) return ATR_E_NOSCENE;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1549,7 +1492,6 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
     P.traced_rays = fr->traced_rays;
     P.error_flag = c->d_error;
     apply_tuning(c, P);
-    const int sched = auto_sched(variant, *cam);
     HIPCHK(hipEventRecord(c->ev_start, s));
     for (int32_t g = 0; g < ngroups; ++g) {
         const int32_t a = g * tiles_per_launch, e = std::min(ntiles, a + tiles_per_launch);

@@ -444,3 +444,142 @@ int32_t atr::balance_shard_tiles(int32_t W, int32_t H, int32_t side, int32_t wor
     }
     return n;
 }
+
+// ------------------------------------------------------------------ device tables of an octree model
+namespace {
+// IEEE binary16 bits of an integer |v| <= 2047 (exact).
+uint16_t half_of_int(int32_t v) {
+    if (v == 0) return 0;
+    const uint32_t sign = v < 0 ? 0x8000u : 0u;
+    uint32_t m = uint32_t(v < 0 ? -v : v);
+    int e = 31 - __builtin_clz(m);
+    return uint16_t(sign | (uint32_t(e + 15) << 10) | ((m << (10 - e)) & 0x3FFu));
+}
+}  // namespace
+
+atr::DTri atr::make_tri(const float* v, uint32_t face) {
+    DTri t;
+    std::memset(&t, 0, sizeof(t));
+    const V3 a = mk(v[0], v[1], v[2]), b = mk(v[3], v[4], v[5]), c = mk(v[6], v[7], v[8]);
+    const V3 ab = sub(b, a), ac = sub(c, a);  // model.h:77-78, once per primitive
+    t.ax = a.x; t.ay = a.y; t.az = a.z;
+    t.abx = ab.x; t.aby = ab.y; t.abz = ab.z;
+    t.acx = ac.x; t.acy = ac.y; t.acz = ac.z;
+    t.face = face;
+    return t;
+}
+
+int atr::pack_tree(const HostTree& T, int cluster_size, PackedTree& P) {
+    P = PackedTree();
+    if (T.nnodes <= 0 || T.bounds.size() != 6 * size_t(T.nnodes) || T.children.size() != size_t(T.nnodes) ||
+        T.parent.size() != size_t(T.nnodes) || T.depth.size() != size_t(T.nnodes) ||
+        T.leaf_first.size() != size_t(T.nnodes) || T.leaf_count.size() != size_t(T.nnodes) ||
+        T.prim_vertices.size() != 9 * T.prim_face.size())
+        return ATR_E_INVALID;
+    const size_t nprims = T.prim_face.size();
+    P.nodes.resize(size_t(T.nnodes));
+    std::vector<uint32_t> range(2 * size_t(T.nnodes), 0);
+    for (int32_t n = 0; n < T.nnodes; ++n) {
+        DNode& d = P.nodes[size_t(n)];
+        const float* b = &T.bounds[6 * size_t(n)];
+        d.lo_x = b[0]; d.lo_y = b[1]; d.lo_z = b[2];
+        d.hi_x = b[3]; d.hi_y = b[4]; d.hi_z = b[5];
+        d.children = T.children[size_t(n)];
+        d.parent = T.parent[size_t(n)];
+        if (!T.children[size_t(n)] && uint64_t(T.leaf_first[size_t(n)]) + T.leaf_count[size_t(n)] > nprims)
+            return ATR_E_INVALID;
+        range[2 * size_t(n)] = T.leaf_first[size_t(n)];
+        range[2 * size_t(n) + 1] = T.children[size_t(n)] ? 0u : T.leaf_count[size_t(n)];
+        P.max_depth = std::max(P.max_depth, T.depth[size_t(n)]);
+    }
+    // leaves are addressed by their static discovery rank on the device (inner_table)
+    std::vector<int32_t> leaf_rank;
+    int rc;
+    if ((rc = inner_table(T, P.inner, leaf_rank))) return rc;
+    P.ninner = int32_t(P.inner.size() / 3);
+    if (P.inner.empty()) P.inner.assign(3, float4_t{0.f, 0.f, 0.f, 0.f});
+    auto by_rank = [&](const std::vector<uint32_t>& per_node) {
+        std::vector<uint32_t> out(std::max<size_t>(2, per_node.size()), 0u);
+        for (int32_t n = 0; n < T.nnodes; ++n) {
+            const int32_t k = leaf_rank[size_t(n)];
+            if (k < 0) continue;
+            out[2 * size_t(k)] = per_node[2 * size_t(n)];
+            out[2 * size_t(k) + 1] = per_node[2 * size_t(n) + 1];
+        }
+        return out;
+    };
+    P.leaf_range = by_rank(range);
+    P.tris.resize(nprims);
+    for (size_t k = 0; k < nprims; ++k) P.tris[k] = make_tri(&T.prim_vertices[9 * k], T.prim_face[k]);
+    const size_t np = nprims ? nprims : 1;
+    P.t0.assign(np, float4_t{0.f, 0.f, 0.f, 0.f});
+    P.t1.assign(np, float4_t{0.f, 0.f, 0.f, 0.f});
+    P.t2.assign(np, 0.f);
+    P.tface.assign(np, 0u);
+    for (size_t k = 0; k < nprims; ++k) {
+        const DTri& t = P.tris[k];
+        P.t0[k] = float4_t{t.ax, t.ay, t.az, t.abx};
+        P.t1[k] = float4_t{t.aby, t.abz, t.acx, t.acy};
+        P.t2[k] = t.acz;
+        P.tface[k] = t.face;
+    }
+    // clustered copy of the leaf primitives
+    LeafClusters C;
+    if ((rc = leaf_clusters(T, cluster_size, C))) return rc;
+    // every cluster owns kMaxClusterSize consecutive slots (its first slot is 16 c), so the
+    // record's last word can carry the screen normals' step instead
+    const size_t ncl = C.rec.size() / 8;
+    P.nclusters = ncl;
+    const size_t ns = std::max<size_t>(1, ncl) * kMaxClusterSize;
+    // full-test records, 48 B per slot (cluster.h load_prim)
+    P.prim.assign(3 * ns, float4_t{0.f, 0.f, 0.f, 0.f});
+    // screen normals, kNormWords u32 per cluster: (nx, ny) of slot k as f16 in word k, then
+    // (nz of slot 2i, nz of slot 2i + 1) in word kMaxClusterSize + i (cluster.h)
+    std::vector<uint32_t> nw(std::max<size_t>(1, ncl) * kNormWords, 0u);
+    for (size_t cl = 0; cl < ncl; ++cl) {
+        uint32_t pw, first;
+        std::memcpy(&pw, &C.rec[8 * cl + 3], 4);
+        std::memcpy(&first, &C.rec[8 * cl + 7], 4);
+        const uint32_t n = (pw & 31u) + 1u;
+        if (n > uint32_t(kMaxClusterSize) || size_t(first) + n > C.order.size()) return ATR_E_INVALID;
+        // screen normals: a step q >= max |n component| / 511 and each normal as round(n / q),
+        // integers of at most 511 (exact in f16; |n - q p| <= q / 2)
+        double mx = 0.0;
+        for (uint32_t k = first; k < first + n; ++k)
+            for (int a = 0; a < 3; ++a) mx = std::max(mx, std::fabs(double(C.normal[3 * size_t(k) + size_t(a)])));
+        float q = float(mx / 511.0);
+        while (double(q) * 511.0 < mx) q = std::nextafter(q, INFINITY);
+        if (!(q > 0.f)) q = 1e-30f;
+        C.rec[8 * cl + 7] = q;
+        for (uint32_t i = 0; i < n; ++i) {
+            const size_t k = first + i, slot = cl * kMaxClusterSize + i;
+            if (C.order[k] >= nprims) return ATR_E_INVALID;
+            const DTri& t = P.tris[C.order[k]];
+            float rk, fc;
+            std::memcpy(&rk, &C.rank[k], 4);
+            std::memcpy(&fc, &t.face, 4);
+            P.prim[3 * slot] = float4_t{t.ax, t.ay, t.az, t.abx};
+            P.prim[3 * slot + 1] = float4_t{t.aby, t.abz, t.acx, t.acy};
+            P.prim[3 * slot + 2] = float4_t{t.acz, rk, fc, 0.f};
+            uint16_t h[3];
+            for (int a = 0; a < 3; ++a) {
+                const double r = double(C.normal[3 * k + size_t(a)]) / double(q);
+                long v = std::isfinite(r) ? std::lround(std::max(-1e6, std::min(1e6, r))) : 0L;
+                v = std::max(-511L, std::min(511L, v));
+                h[a] = half_of_int(int32_t(v));
+            }
+            nw[kNormWords * cl + i] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
+            nw[kNormWords * cl + kMaxClusterSize + i / 2] |= uint32_t(h[2]) << (16 * (i & 1));
+        }
+    }
+    // one 128-B block per cluster: record {lo, P}{hi, q}, then its kNormWords normal words
+    static_assert(8 + kNormWords == 4 * kClusterBlock, "cluster block layout");
+    P.clus.assign(std::max<size_t>(1, ncl) * 4 * kClusterBlock, 0u);
+    for (size_t cl = 0; cl < ncl; ++cl) {
+        std::memcpy(&P.clus[4 * kClusterBlock * cl], &C.rec[8 * cl], 8 * sizeof(float));
+        std::memcpy(&P.clus[4 * kClusterBlock * cl + 8], &nw[kNormWords * cl], kNormWords * sizeof(uint32_t));
+    }
+    P.cl_range = by_rank(C.range);
+    P.near_ok = P.max_depth <= 8 && P.ninner < 65536;  // traverse_pass_near's register stack
+    return ATR_OK;
+}

@@ -47,6 +47,28 @@ int leaf_clusters(const HostTree& T, int size, LeafClusters& C);
 // the leaf's rank in the static discovery order (-1 for inner nodes): leaf ids on the device.
 int inner_table(const HostTree& T, std::vector<float4_t>& out, std::vector<int32_t>& leaf_rank);
 
+// The device tables of one octree model (atr_scene_upload), built on the host: every array the
+// kernels index, in the layouts of DESIGN.md §3. Kept apart from the upload so the sanitizer
+// harness (tests/c/host_sanitize.cpp) checks the packing's sizes and index ranges.
+struct PackedTree {
+    std::vector<DNode> nodes;          // reference node order (LANE)
+    std::vector<uint32_t> leaf_range;  // 2 per leaf rank: first leaf-ordered primitive, count
+    std::vector<float4_t> inner;       // inner_table, 3 per inner node
+    int32_t ninner = 0;
+    std::vector<DTri> tris;            // leaf-ordered primitives, ab / ac precomputed (model.h:77-78)
+    std::vector<float4_t> t0, t1;      // LANE's SoA streams of `tris`
+    std::vector<float> t2;
+    std::vector<uint32_t> tface;
+    size_t nclusters = 0;
+    std::vector<uint32_t> clus;        // 4 x kClusterBlock u32 per cluster: {lo, P}{hi, q}, normal words
+    std::vector<uint32_t> cl_range;    // 2 per leaf rank: first cluster, cluster count
+    std::vector<float4_t> prim;        // 3 per slot (kMaxClusterSize slots per cluster): 48-B records
+    int32_t max_depth = 0;
+    bool near_ok = false;              // traverse_pass_near's register stack fits the tree
+};
+int pack_tree(const HostTree& T, int cluster_size, PackedTree& P);
+DTri make_tri(const float* v9, uint32_t face);
+
 // load_model_data (OBJ_loader.cpp:278-360) on `threads` newline-aligned chunks (obj_parse.cpp);
 // the result does not depend on `threads`.
 int parse_obj_text(const char* text, size_t len, HostMesh& m, int threads = 1);

@@ -111,7 +111,7 @@ EXPORTS = [
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_default_tuning", "atr_set_tuning", "atr_get_tuning", "atr_pack_bgr", "atr_scatter_bgr",
-    "atr_render_plan_info",
+    "atr_render_plan_info", "atr_workspace_info",
 ]
 # the diagnostic build's extra symbols (include/atray_diag.h; make -C atray_amd/csrc DIAG=1)
 DIAG_EXPORTS = ["atr_render_wave_trace", "atr_render_phase_clocks", "atr_render_path_counters",
@@ -157,6 +157,7 @@ def lib():
         "atr_version": ([], C.c_char_p),
         "atr_scene_upload": ([vp, vp, i32, vp, i32, vp, i32, vp, i32], C.c_int),
         "atr_scene_info": ([vp, P(i64), P(i32), P(i32)], C.c_int),
+        "atr_workspace_info": ([vp, P(i32), P(i64)], C.c_int),
         "atr_render_start": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp], C.c_int),
         "atr_render_start_ex": ([vp, P(atr_camera), vp, i32, P(atr_frame), C.c_uint64, vp, i32], C.c_int),
         "atr_render_packed_size": ([vp, i32], i64),
@@ -433,6 +434,12 @@ class Engine:
                                      C.cast(sph, C.c_void_p), len(spheres),
                                      C.cast(pln, C.c_void_p), len(planes)), "scene upload")
         self._keep = [materials, models]
+
+    def workspace_info(self):
+        """Path-engine workspaces held (count, device bytes): atr_workspace_info."""
+        n, b = C.c_int32(), C.c_int64()
+        check(lib().atr_workspace_info(self.h, C.byref(n), C.byref(b)))
+        return {"workspaces": n.value, "device_bytes": b.value}
 
     def scene_info(self):
         b, n, d = C.c_int64(), C.c_int32(), C.c_int32()

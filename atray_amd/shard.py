@@ -71,6 +71,29 @@ def tile_costs(eng, cam, width: int, height: int, side: int, seed: int) -> np.nd
     return eng.tile_costs(cam, E.shard_grid(width, height, side), seed)
 
 
+GRADE_BOUNDS = (0.02, 0.05, 0.10, 0.20, 0.30, 0.50, 0.75)  # cumulative fractions, heaviest first
+
+
+def graded_cell_plan(cell_costs, prio_frac: float = 0.0) -> np.ndarray:
+    """atr_set_cell_plan bytes that dispatch cells by measured cost, heaviest class first: class 7
+    (bits 4-6) for the top 2 % of the cells that cost anything, 6 for the next to 5 %, ..., 0 for the
+    rest (the single-frame plan's fractions, plan.hip); prio_frac: the heaviest cells' waves also
+    issue at raised priority (ATR_PLAN_PRIO, 0x80). Scheduling only: outputs never change."""
+    cc = np.asarray(cell_costs).ravel()
+    order = np.argsort(-cc, kind="stable")
+    live = int((cc > 0).sum())
+    crank = np.empty(cc.size, np.int64)
+    crank[order] = np.arange(cc.size)
+    cls = np.zeros(cc.size, np.uint8)
+    for k, f in enumerate(GRADE_BOUNDS):
+        cls[crank >= int(round(f * live))] = 6 - k
+    cls[crank < int(round(GRADE_BOUNDS[0] * live))] = 7
+    plan = (cls << 4).astype(np.uint8)
+    if prio_frac > 0:
+        plan[crank < int(round(prio_frac * live))] |= 0x80
+    return plan
+
+
 def shared_costs(costs, rank: int, dist, device):
     """Rank 0's measured costs on every rank (timings differ per GPU; the plan must not)."""
     import torch

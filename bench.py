@@ -533,18 +533,8 @@ def run(args):
             nsplit = int(round(float(frac) * cc.size))
             cplan[corder[:nsplit]] = int(parts)
             cell_split.update(parts=int(parts), cells=nsplit)
-        if args.cell_order != "list":
-            live = int((cc > 0).sum())
-            bounds = [0.02, 0.05, 0.10, 0.20, 0.30, 0.50, 0.75]  # cumulative, heaviest first
-            cls = np.zeros(cc.size, np.uint8)
-            crank = np.empty(cc.size, np.int64)
-            crank[corder] = np.arange(cc.size)
-            for k, f in enumerate(bounds):  # class 7 for the top 2 %, ..., 0 for the rest
-                cls[crank >= int(round(f * live))] = 6 - k
-            cls[crank < int(round(bounds[0] * live))] = 7
-            cplan |= (cls << 4).astype(np.uint8)
-            if args.cell_prio > 0:  # the heaviest cells' waves also issue first on their SIMD
-                cplan[crank < int(round(args.cell_prio * live))] |= 0x80  # ATR_PLAN_PRIO
+        if args.cell_order != "list":  # class 7 for the top 2 %, ..., 0 for the rest; --cell-prio:
+            cplan |= S.graded_cell_plan(cc, args.cell_prio)  # the heaviest cells' waves issue first
             cell_split["order"] = args.cell_order
             cell_split["prio_frac"] = args.cell_prio
         eng.set_cell_plan(W, H, cplan)

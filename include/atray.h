@@ -190,6 +190,12 @@ int atr_scene_upload(atr_ctx* ctx, const atr_material* materials, int32_t nmater
                      int32_t nspheres, const atr_plane* planes, int32_t nplanes);
 /* device bytes of the uploaded scene, per-model node count and max tree depth */
 int atr_scene_info(atr_ctx* ctx, int64_t* device_bytes, int32_t* max_nodes, int32_t* max_depth);
+/* Path-engine workspaces held by the context (PATHS: two path queues + per-path results, 144 B per
+   path of a batch): how many (at most 4, whatever the number of streams rendering: a stream without
+   one takes an idle or the least recently used one) and their device bytes. When the device cannot
+   hold a batch's workspace the engine halves the batch (down to 2^16 paths), then renders on FLAT,
+   which needs none; outputs are identical either way. */
+int atr_workspace_info(atr_ctx* ctx, int32_t* workspaces, int64_t* device_bytes);
 
 /* Output layout of a render. IMAGE: pixel (x,y) at y*width + x. PACKED: the pixels of the
    render's work blocks back to back (atr_render_packed_size); atr_unpack scatters them. */

@@ -6,10 +6,12 @@
 //   parse_obj_text  (load_model_data, OBJ_loader.cpp:278-360) at 1, 3 and 8 threads -- the meshes
 //                   must be identical;
 //   mesh_aabb / mesh_translate, octree_build (build_oct_kd_tree, kd_tree.cpp:67-288),
-//   octree_finish, octree_stats, leaf_clusters (8 and 16 slots), inner_table;
+//   octree_finish, octree_stats, leaf_clusters (8 and 16 slots), inner_table, pack_tree (the
+//   device tables atr_scene_upload uploads: sizes and every stored index checked);
 //   reference_tiles (renderer.cpp:403-455), shard_tiles, balance_shard_tiles, camera_set.
 // A sanitizer report aborts the process (halt_on_error); the final line "host_sanitize ok N"
 // says how many cases ran.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,6 +47,52 @@ bool same_mesh(const HostMesh& a, const HostMesh& b) {
 
 bool g_verbose = false;
 
+uint32_t bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+// pack_tree (atr_scene_upload's device tables): every array sized as the kernels assume and every
+// stored index inside the table it indexes.
+void pack_case(const HostTree& T, size_t nfaces, int cluster_size) {
+    PackedTree P;
+    if (pack_tree(T, cluster_size, P) != ATR_OK) return;  // ATR_E_TREE_LAYOUT and the like
+    ++g_cases;
+    const size_t nprims = T.prim_face.size(), ncl = P.nclusters, nleafr = P.leaf_range.size() / 2;
+    CHECK(P.nodes.size() == size_t(T.nnodes));
+    CHECK(P.inner.size() == 3 * size_t(std::max(1, P.ninner)));
+    CHECK(P.tris.size() == nprims && P.t0.size() == std::max<size_t>(1, nprims) && P.t1.size() == P.t0.size() &&
+          P.t2.size() == P.t0.size() && P.tface.size() == P.t0.size());
+    CHECK(P.clus.size() == std::max<size_t>(1, ncl) * 4 * kClusterBlock);
+    CHECK(P.prim.size() == 3 * std::max<size_t>(1, ncl) * kMaxClusterSize);
+    CHECK(P.cl_range.size() == P.leaf_range.size() && P.leaf_range.size() >= 2);
+    for (size_t k = 0; k < nleafr; ++k) {
+        CHECK(uint64_t(P.leaf_range[2 * k]) + P.leaf_range[2 * k + 1] <= nprims);
+        CHECK(uint64_t(P.cl_range[2 * k]) + P.cl_range[2 * k + 1] <= ncl);
+    }
+    for (size_t c = 0; c < ncl; ++c) {
+        const uint32_t n = (P.clus[4 * kClusterBlock * c + 3] & 31u) + 1u;
+        CHECK(n <= uint32_t(cluster_size) && n <= uint32_t(kMaxClusterSize));
+        for (uint32_t i = 0; i < n; ++i) {
+            const float4_t r = P.prim[3 * (c * kMaxClusterSize + i) + 2];
+            CHECK(bits(r.z) < nfaces);                  // face id
+            CHECK(bits(r.y) < uint32_t(1u << 30));      // leaf rank of the primitive
+        }
+        for (uint32_t i = n; i < uint32_t(kMaxClusterSize); ++i) {  // unused slots stay zero
+            const float4_t r = P.prim[3 * (c * kMaxClusterSize + i) + 2];
+            CHECK(bits(r.y) == 0 && bits(r.z) == 0);
+        }
+    }
+    for (int32_t i = 0; i < P.ninner; ++i) {
+        const float4_t w = P.inner[3 * size_t(i) + 2];
+        CHECK(bits(w.y) < uint32_t(std::max<size_t>(1, nleafr)));              // first leaf child's rank
+        CHECK(int32_t(bits(w.z)) >= -1 && int32_t(bits(w.z)) < P.ninner);      // parent inner id
+        CHECK((bits(w.w) >> 8) < uint32_t(P.ninner));                           // first inner child id
+    }
+    CHECK(P.near_ok == (P.max_depth <= 8 && P.ninner < 65536));
+}
+
 void scene_case(const std::string& text, uint32_t max_faces) {
     ++g_cases;
     if (g_verbose) std::fprintf(stderr, "case %d: %zu bytes, max_faces %u\n", g_cases, text.size(), max_faces);
@@ -67,6 +115,7 @@ void scene_case(const std::string& text, uint32_t max_faces) {
     std::vector<float4_t> inner;
     std::vector<int32_t> leaf_rank;
     inner_table(T, inner, leaf_rank);
+    for (int size : {16, 5}) pack_case(T, m1.nfaces(), size);
     if (!m1.vertices.empty()) {
         mesh_translate(m1, box, mk(1.f, -2.f, 3.f));
         mesh_aabb(m1, box);

@@ -175,6 +175,66 @@ def test_per_frame_cameras_equal_single_renders(eng, variant, spp, bounces, layo
     assert not torch.equal(fb[:n], fb[stride:stride + n])
 
 
+def test_c3_timed_shape_launch(eng, oracle_scene):
+    """The bench's timed c3 launch shape (bench.py run(): atr_render_start_cameras, 10 orbit
+    cameras at 1920x1080, 1 spp, 1 bounce -> the 7-wave HYBRID primary kernel of multi-frame
+    launches, graded cell order from calibration frames), with the app camera as one of the frames:
+      * that frame reproduces the reference hash 43ad95dbe7a70300 with 284,360 hits (SURVEY 8(c));
+      * every other frame equals its one-camera render (the 6-wave single-frame kernel);
+      * one row band per frame matches the oracle (renderer.cpp:294-369, kd_tree.cpp:337-465).
+    Round 4's only GPU fault (an illegal address in a reverted change) happened
+    at this shape, which no test covered."""
+    import bench
+    from atray_amd import shard as S
+    W, H, F, APP = 1920, 1080, 10, 4
+    eyes = [bench.orbit_eye(5 + f) for f in range(F)]
+    eyes[APP] = bench.APP_EYE  # app.cpp:81-88
+    cams = [E.camera(W, H, 1, 1, eye=e, facing=bench.APP_FACING) for e in eyes]
+    # the bench's graded cell order, calibrated on the three orbit frames before the window
+    cc = sum(eng.cell_costs(E.camera(W, H, 1, 1, eye=bench.orbit_eye(k), facing=bench.APP_FACING), SEED)
+             for k in (2, 3, 4))
+    eng.set_cell_plan(W, H, S.graded_cell_plan(cc))
+    n = W * H
+    dev = torch.device("cuda", 0)
+    try:
+        fb = torch.full((F * n,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
+        face = torch.full((F * n,), -7, dtype=torch.int32, device=dev)
+        t = torch.zeros(F * n, dtype=torch.float32, device=dev)
+        casts = torch.full((F * n,), -1, dtype=torch.int32, device=dev)
+        traced = torch.zeros(1, dtype=torch.int64, device=dev)
+        fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), face.data_ptr(), t.data_ptr(), None, casts.data_ptr(),
+                         traced.data_ptr())
+        torch.cuda.synchronize()
+        eng.render_start_cameras(cams, [[0, 0, W - 1, H - 1]], fr, n, SEED,
+                                 stream=torch.cuda.current_stream().cuda_stream)
+        assert eng.wait()[0] == 0
+        torch.cuda.synchronize()
+        assert int(traced.item()) == F * n
+        fa = face[APP * n:(APP + 1) * n].cpu().numpy().view(np.uint32).reshape(H, W)
+        ta = t[APP * n:(APP + 1) * n].cpu().numpy().reshape(H, W)
+        assert int((fa != E.MISS).sum()) == 284360
+        assert f"{O.fnv_hits(fa, ta):016x}" == "43ad95dbe7a70300"
+        for f, cam in enumerate(cams):
+            eng.set_cell_plan(W, H, None)  # the one-camera renders: the single-frame plan
+            one = render(eng, cam, E.ATR_KERNEL_AUTO, with_rgb=False)
+            sl = slice(f * n, (f + 1) * n)
+            assert torch.equal(fb[sl].view(H, W), one["fb"]), f
+            assert torch.equal(casts[sl].view(H, W), one["casts"]), f
+            assert torch.equal(face[sl].view(H, W), one["face"]), f
+            assert torch.equal(t[sl].view(torch.int32).view(H, W), one["t"].view(torch.int32)), f
+            # one oracle band per frame, through the dragon (rows 300-700 hold it on the orbit)
+            y0 = 320 + 37 * f
+            ocam = O.Camera(W, H, eye=eyes[f], facing=bench.APP_FACING)
+            of, ot, _ = oracle_scene.primary_hits(ocam, y0, y0 + 2)
+            assert np.array_equal(face[sl].view(H, W)[y0:y0 + 2].cpu().numpy().view(np.uint32), of), f
+            assert np.array_equal(t[sl].view(H, W)[y0:y0 + 2].cpu().numpy().view(np.uint32), ot.view(np.uint32)), f
+            _, ofb, ocasts, _ = oracle_scene.render(ocam, SEED, y0, y0 + 2)
+            assert np.array_equal(fb[sl].view(H, W)[y0:y0 + 2].cpu().numpy().view(np.uint32), ofb), f
+            assert np.array_equal(casts[sl].view(H, W)[y0:y0 + 2].cpu().numpy().view(np.uint32), ocasts), f
+    finally:
+        eng.set_cell_plan(W, H, None)
+
+
 def test_per_frame_cameras_reject_mismatched_settings(eng):
     W, H = 64, 32
     a, b = E.camera(W, H, 1, 1), E.camera(W, H, 2, 1)
