@@ -1,0 +1,274 @@
+// bounce_sim.cpp -- offline work model of the clustered scan for BOUNCE rays (analysis tool, not
+// product). Where do a bounce ray's full triangle tests go?
+//
+// Builds the Dragon surrogate's octree and leaf clusters with the product's host code, traces the
+// camera rays of every `step`-th pixel of a 1920x1080 frame, and from each hit one bounce ray per
+// sample (the reference's bounce: renderer.cpp:231-258 with the interpolated normal replaced by
+// the geometric one, a PCG-like hash for the three rand_bi draws). Each bounce ray is traced with
+// the kernel's clustered scan (loose + tight padded boxes, det screen; the reference leaf order)
+// and every full test is classified:
+//   hit       accepted (t > kTol, u, v in range)
+//   behind    plane parameter t <= kTol (the triangle's plane is at or behind the origin: the
+//             origin's own surface patch)
+//   far       plane t beyond the best t so far
+//   uv        plane t in (kTol, best) but the line misses the triangle (u, v out of range)
+//   culled    det below kTol (the screen's band kept it)
+// and the would-be rejections of cheaper per-primitive screens are counted: the plane test with
+// f32 normals (behind / far) and a bounding sphere around the triangle.
+//
+// g++ -O2 -std=c++17 -ffp-contract=off -I atray_amd/csrc tools/bounce_sim.cpp
+//     atray_amd/csrc/host_scene.cpp -o build/bounce_sim && build/bounce_sim OBJ [step] [spp]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <vector>
+
+#include "engine.h"
+#include "host_scene.h"
+
+using namespace atr;
+
+namespace {
+
+struct TriOut { float t, u, v, det; bool acc; };
+TriOut tri(V3 o, V3 d, V3 a, V3 ab, V3 ac) {
+    TriOut r{0, 0, 0, 0, false};
+    const V3 pvec = cross(d, ac);
+    r.det = dot(ab, pvec);
+    if (r.det < kTol) return r;
+    const float det_inv = 1 / r.det;
+    const V3 tvec = sub(o, a);
+    r.u = dot(tvec, pvec) * det_inv;
+    const V3 qvec = cross(tvec, ab);
+    r.v = dot(d, qvec) * det_inv;
+    r.t = dot(qvec, ac) * det_inv;
+    r.acc = !(r.u < 0 || r.u > 1 || r.v < 0 || r.u + r.v > 1);
+    return r;
+}
+
+bool box_check(V3 o, V3 inv, const float* b) {
+    const int s0 = inv.x < 0, s1 = inv.y < 0, s2 = inv.z < 0;
+    float tmin = ((s0 ? b[3] : b[0]) - o.x) * inv.x, tmax = ((s0 ? b[0] : b[3]) - o.x) * inv.x;
+    const float tymin = ((s1 ? b[4] : b[1]) - o.y) * inv.y, tymax = ((s1 ? b[1] : b[4]) - o.y) * inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((s2 ? b[5] : b[2]) - o.z) * inv.z, tzmax = ((s2 ? b[2] : b[5]) - o.z) * inv.z;
+    return !((tmin > tzmax) || (tzmin > tmax));
+}
+float box_entry(V3 o, V3 inv, const float* b) {
+    const int s0 = inv.x < 0, s1 = inv.y < 0, s2 = inv.z < 0;
+    float tmin = ((s0 ? b[3] : b[0]) - o.x) * inv.x, tmax = ((s0 ? b[0] : b[3]) - o.x) * inv.x;
+    const float tymin = ((s1 ? b[4] : b[1]) - o.y) * inv.y, tymax = ((s1 ? b[1] : b[4]) - o.y) * inv.y;
+    if ((tmin > tymax) || (tymin > tmax)) return 0;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    const float tzmin = ((s2 ? b[5] : b[2]) - o.z) * inv.z, tzmax = ((s2 ? b[2] : b[5]) - o.z) * inv.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return 0;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    if (tmin > 0) return tmin;
+    if (tmax > 0) return tmax;
+    return 0;
+}
+
+uint64_t hash64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return x;
+}
+float rbi(uint64_t& s) { s = hash64(s + 0x9E3779B97F4A7C15ull); return float(s >> 40) / float(1 << 24) * 2.f - 1.f; }
+
+struct Cls { double rays = 0, leaves = 0, crec = 0, cpass = 0, screen = 0, full = 0, hit = 0, behind = 0, far = 0,
+             uv = 0, culled = 0, plane_keep = 0, sphere_keep = 0, both_keep = 0, origin_leaf_full = 0; };
+
+struct Scene {
+    HostTree T;
+    LeafClusters C;
+    std::vector<float> sph;  // per slot: bounding sphere centre + radius (f32, exact enough for a model)
+};
+
+// One query with the kernel's clustered scan; returns best t (kMaxFloat none) and the hit slot.
+float trace(const Scene& S, V3 o, V3 d, Cls* cls, uint32_t& hit_slot) {
+    const HostTree& T = S.T;
+    const LeafClusters& C = S.C;
+    const V3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+    hit_slot = 0xFFFFFFFFu;
+    if (cls) cls->rays += 1;
+    if (!box_check(o, inv, &T.bounds[0])) return kMaxFloat;
+    std::vector<std::pair<float, int>> leaves;
+    std::vector<int32_t> stack(1, 0);
+    while (!stack.empty()) {
+        const int32_t cur = stack.back();
+        stack.pop_back();
+        const int32_t ch = T.children[size_t(cur)];
+        int hit = 0;
+        for (int i = 0; i < 8 && hit <= 4; ++i) {
+            const int32_t c = ch + i;
+            if (T.children[size_t(c)]) {
+                if (box_check(o, inv, &T.bounds[6 * size_t(c)])) { ++hit; stack.push_back(c); }
+            } else {
+                const float dis = box_entry(o, inv, &T.bounds[6 * size_t(c)]);
+                if (dis > 0) {
+                    ++hit;
+                    auto it = std::upper_bound(leaves.begin(), leaves.end(), dis,
+                                               [](float v, const std::pair<float, int>& e) { return v < e.first; });
+                    leaves.insert(it, {dis, c});
+                }
+            }
+        }
+    }
+    float best = kMaxFloat;
+    bool first_leaf = true;
+    for (auto& lf : leaves) {
+        if (cls) cls->leaves += 1;
+        const uint32_t c0 = C.range[2 * size_t(lf.second)], nc = C.range[2 * size_t(lf.second) + 1];
+        bool improved = false;
+        for (uint32_t c = c0; c < c0 + nc; ++c) {
+            if (cls) cls->crec += 1;
+            const float* r = &C.rec[8 * size_t(c)];
+            const float eps = 5.9604645e-8f, tau = 3e-3f;
+            const float ex = r[4] - r[0], ey = r[5] - r[1], ez = r[6] - r[2];
+            const float fx = std::max(std::fabs(r[0] - o.x), std::fabs(r[4] - o.x));
+            const float fy = std::max(std::fabs(r[1] - o.y), std::fabs(r[5] - o.y));
+            const float fz = std::max(std::fabs(r[2] - o.z), std::fabs(r[6] - o.z));
+            const float W = std::sqrt(fx * fx + fy * fy + fz * fz) * 1.0000005f + (ex + ey + ez);
+            const float P = r[3];
+            auto pad = [&](float D) { return W * (P * (36 * eps / (0.9f * D)) + 12 * eps); };
+            auto hitbox = [&](float g) {
+                float bb[6];
+                for (int q = 0; q < 3; ++q) { bb[q] = r[q] - g; bb[3 + q] = r[4 + q] + g; }
+                return box_check(o, inv, bb) && !(box_entry(o, inv, bb) > best);
+            };
+            const float mg = 16 * eps * P;
+            const float dlo = kTol - mg;
+            float dhi = 1e30f;
+            if (!hitbox(pad(kTol))) continue;
+            if (!hitbox(pad(tau))) dhi = tau + mg;
+            if (cls) cls->cpass += 1;
+            uint32_t pw, fs;
+            std::memcpy(&pw, &C.rec[8 * c + 3], 4);
+            std::memcpy(&fs, &C.rec[8 * c + 7], 4);
+            const uint32_t n = (pw & 31u) + 1u;
+            for (uint32_t k = fs; k < fs + n; ++k) {
+                if (cls) cls->screen += 1;
+                const float* nn = &C.normal[3 * k];
+                const float det = -(d.x * nn[0] + d.y * nn[1] + d.z * nn[2]);
+                if (!(det >= dlo && det < dhi)) continue;
+                const float* v = &T.prim_vertices[9 * size_t(C.order[k])];
+                const V3 a = mk(v[0], v[1], v[2]);
+                const TriOut to = tri(o, d, a, sub(mk(v[3], v[4], v[5]), a), sub(mk(v[6], v[7], v[8]), a));
+                const bool accepted = to.det >= kTol && to.acc && to.t > kTol && to.t < best;
+                if (cls) {
+                    cls->full += 1;
+                    if (first_leaf) cls->origin_leaf_full += 1;
+                    // plane parameter in double
+                    const double n0 = nn[0], n1 = nn[1], n2 = nn[2];
+                    const double num = (double(a.x) - o.x) * n0 + (double(a.y) - o.y) * n1 + (double(a.z) - o.z) * n2;
+                    const double den = double(d.x) * n0 + double(d.y) * n1 + double(d.z) * n2;
+                    const double tp = den != 0 ? num / den : 1e30;
+                    if (to.det < kTol) cls->culled += 1;
+                    else if (accepted || (to.acc && to.t > kTol)) cls->hit += 1;
+                    else if (tp <= kTol) cls->behind += 1;
+                    else if (tp >= best) cls->far += 1;
+                    else cls->uv += 1;
+                    // would a per-primitive plane screen keep it? (margin 1e-5 relative + 1e-6)
+                    const bool pk = !(tp <= kTol * 0.5 || tp > double(best) * 1.001 + 1e-5);
+                    // bounding sphere (f32 centre, radius + rounding pad): does the line pass within R?
+                    const float* sp = &S.sph[4 * size_t(k)];
+                    const double w[3] = {sp[0] - double(o.x), sp[1] - double(o.y), sp[2] - double(o.z)};
+                    const double tc = w[0] * d.x + w[1] * d.y + w[2] * d.z;
+                    const double cx = w[1] * d.z - w[2] * d.y, cy = w[2] * d.x - w[0] * d.z, cz = w[0] * d.y - w[1] * d.x;
+                    const double R = sp[3] * 1.001 + pad(det >= tau ? tau : kTol);
+                    const bool sk = cx * cx + cy * cy + cz * cz <= R * R && tc + R > kTol && tc - R < best;
+                    cls->plane_keep += pk;
+                    cls->sphere_keep += sk;
+                    cls->both_keep += pk && sk;
+                }
+                if (accepted) { best = to.t; hit_slot = k; improved = true; }
+            }
+        }
+        first_leaf = false;
+        if (improved) break;
+    }
+    return best;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) { std::fprintf(stderr, "usage: bounce_sim OBJ [step] [spp]\n"); return 2; }
+    const int step = argc > 2 ? std::atoi(argv[2]) : 8;
+    const int spp = argc > 3 ? std::atoi(argv[3]) : 4;
+    std::ifstream f(argv[1], std::ios::binary);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string text = ss.str();
+    HostMesh M;
+    if (parse_obj_text(text.data(), text.size(), M)) return 1;
+    float box[6];
+    mesh_aabb(M, box);
+    mesh_translate(M, box, mk(0.f, -15.f, -38.f));
+    Scene S;
+    if (octree_build(M, 300, S.T)) return 1;
+    if (leaf_clusters(S.T, 16, S.C)) return 1;
+    const size_t nslots = S.C.order.size();
+    S.sph.resize(4 * nslots);
+    for (size_t k = 0; k < nslots; ++k) {
+        const float* v = &S.T.prim_vertices[9 * size_t(S.C.order[k])];
+        double cc[3], rr = 0;
+        for (int q = 0; q < 3; ++q) cc[q] = (double(v[q]) + v[3 + q] + v[6 + q]) / 3.0;
+        for (int j = 0; j < 3; ++j) {
+            double d2 = 0;
+            for (int q = 0; q < 3; ++q) d2 += (v[3 * j + q] - cc[q]) * (v[3 * j + q] - cc[q]);
+            rr = std::max(rr, std::sqrt(d2));
+        }
+        for (int q = 0; q < 3; ++q) S.sph[4 * k + q] = float(cc[q]);
+        S.sph[4 * k + 3] = float(rr);
+    }
+    atr_camera cm;
+    camera_set(cm, mk(0.1f, 2.f, 0.f), mk(-0.1f, -0.5f, -1.f), 1920, 1080, 0, 1, 1, 1.f);
+    const V3 eye = from(cm.eye), fc = from(cm.frame_center), cx = from(cm.camera_x), cy = from(cm.camera_y);
+    Cls cam, b1, b2;
+    for (int y = 0; y < cm.height; y += step)
+        for (int x = 0; x < cm.width; x += step) {
+            const float film_y = -1.0f + 2.0f * (float(y) / float(cm.height));
+            const float film_x = ((-1.0f + 2.0f * (float(x) / float(cm.width))) * cm.h_fov) * cm.aspect_ratio;
+            const V3 d0 = unit(sub(add(add(fc, scale(cx, film_x)), scale(cy, film_y)), eye));
+            uint32_t slot;
+            const float t0 = trace(S, eye, d0, &cam, slot);
+            if (slot == 0xFFFFFFFFu) continue;
+            for (int s = 0; s < spp; ++s) {
+                uint64_t st = hash64((uint64_t(y) << 32) ^ uint64_t(x) ^ (uint64_t(s) << 48));
+                V3 o = add(eye, scale(d0, t0)), d = d0;
+                uint32_t sl = slot;
+                for (int level = 1; level <= 2; ++level) {
+                    const float* nn = &S.C.normal[3 * sl];
+                    V3 n = unit(mk(nn[0], nn[1], nn[2]));
+                    if (dot(neg(d), n) < 0) n = neg(n);
+                    const V3 rnd = unit(add(mk(rbi(st), rbi(st), rbi(st)), n));
+                    const V3 pure = unit(sub(d, scale(n, 2 * dot(d, n))));
+                    d = unit(add(scale(rnd, 0.7f), scale(pure, 0.3f)));  // lerp(rnd, pure, 0.3)
+                    const float t = trace(S, o, d, level == 1 ? &b1 : &b2, sl);
+                    if (sl == 0xFFFFFFFFu) break;
+                    o = add(o, scale(d, t));
+                }
+            }
+        }
+    auto pr = [](const char* name, const Cls& c) {
+        const double a = c.rays;
+        std::printf("%-8s rays %.0f: leaves %.2f  cluster recs %.1f  passed %.1f  screened %.1f  full %.1f"
+                    " [hit %.2f behind %.1f far %.1f uv %.1f culled %.2f; origin leaf %.1f]"
+                    "  plane screen keeps %.2f, sphere keeps %.2f, both %.2f\n",
+                    name, a, c.leaves / a, c.crec / a, c.cpass / a, c.screen / a, c.full / a, c.hit / a, c.behind / a,
+                    c.far / a, c.uv / a, c.culled / a, c.origin_leaf_full / a, c.plane_keep / a, c.sphere_keep / a,
+                    c.both_keep / a);
+    };
+    pr("camera", cam);
+    pr("bounce1", b1);
+    pr("bounce2", b2);
+    return 0;
+}
