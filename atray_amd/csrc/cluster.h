@@ -105,6 +105,35 @@ __device__ __forceinline__ bool cluster_pads(const Ray& r, const ScreenRay& sr, 
 // Bit j set iff the f16 dot D_j of slot g + j lies in (blo, ahi]: the det band mapped back through
 // the cluster's step by the caller (cluster_cands). (The slots past n are masked off once per
 // cluster by the caller, not per primitive.)
+#ifndef ATR_SCREEN_TWO_CMP
+// The band as one comparison: |D - mid| <= half. mid enters as the z dot's accumulator, so each
+// primitive costs two dots and one compare (|.| is an operand modifier). Every dot D lies within
+// +-3 x 511 x 1.0005 < 1600 (f16 direction, integer normals of at most 511), so the band is first
+// clipped to [-1600, 1600] -- the tight band (blo = -inf) and bands beyond every D keep exactly
+// the D they kept -- which also bounds mid and half. half covers the closed band plus the
+// rounding of mid and of the accumulation with mid in it (<= 2^-22 (1600 + |mid|)): the screen
+// only grows. An empty band stays empty (half < 0); NaN ends open the band.
+__device__ __forceinline__ void screen_band(float blo, float ahi, float& mid, float& half) {
+    const float lo = fmaxf(blo, -1600.0f), hi = fminf(ahi, 1600.0f);
+    mid = 0.5f * (lo + hi);
+    half = 0.5f * (hi - lo) * 1.000001f + (fabsf(mid) + 2048.0f) * 4.7683716e-7f;  // 2^-21
+}
+__device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float nmid, float half, uint4_t a0, uint4_t a1,
+                                            uint4_t z) {
+    const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t zz[4] = {z.x, z.y, z.z, z.w};
+    uint32_t gc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const h2_t pxy = __builtin_bit_cast(h2_t, xy[j]), pz = __builtin_bit_cast(h2_t, zz[j / 2]);
+        float dz;
+        asm("v_dot2_f32_f16 %0, %1, %2, %3" : "=v"(dz) : "v"((j & 1) ? sr.dz_hi : sr.dz_lo), "v"(pz), "v"(nmid));
+        const float e = __builtin_amdgcn_fdot2(sr.dxy, pxy, dz, false);
+        if (fabsf(e) <= half) gc |= 1u << j;
+    }
+    return gc;
+}
+#else
 __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float blo, float ahi, uint4_t a0, uint4_t a1,
                                             uint4_t z) {
     const uint32_t xy[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -122,6 +151,7 @@ __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float blo, floa
     }
     return gc;
 }
+#endif
 
 // Cluster c of a leaf: the padded box tests and the screen against the bound `best`. Returns the
 // mask of the primitives (slot 16 c + bit) that still need the full test.
@@ -152,8 +182,15 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
     const float ahi = a + fabsf(a) * 9.5367432e-7f + 1.1754944e-38f;
     const float blo = b - fabsf(b) * 9.5367432e-7f - 1.1754944e-38f;
     uint32_t cand = 0;
+#ifndef ATR_SCREEN_TWO_CMP
+    float mid, half;
+    screen_band(blo, ahi, mid, half);
     for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
+        cand |= screen8(sr, -mid, half, nb[g / 4], nb[g / 4 + 1], nb[kMaxClusterSize / 4 + g / 8]) << g;
+#else
+    for (uint32_t g = 0; g < n; g += 8)
         cand |= screen8(sr, blo, ahi, nb[g / 4], nb[g / 4 + 1], nb[kMaxClusterSize / 4 + g / 8]) << g;
+#endif
     return cand & slots;
 }
 

@@ -318,8 +318,13 @@ __device__ __forceinline__ Inner load_inner_uniform(const float4_t* __restrict__
     const float4_t* p = reinterpret_cast<const float4_t*>(u64);
     u32x8_t a;
     u32x4_t c;
+    // early-clobber outputs ("=&s"): the first load's destination must not share registers with
+    // the address the second load reads. Without them the compiler may allocate a over p (it
+    // did: s_load_dwordx8 s[12:19], s[12:13] then s_load_dwordx4 ..., s[12:13]); a fast return
+    // of the first load then turned the second's address into loaded data -- the rare
+    // MEMORY_APERTURE_VIOLATION of rounds 4 and 5
     asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(a), "=s"(c)
+                 : "=&s"(a), "=&s"(c)
                  : "s"(p));
     Inner n;
     n.lx = __uint_as_float(a[0]); n.ly = __uint_as_float(a[1]); n.lz = __uint_as_float(a[2]);

@@ -89,7 +89,24 @@ struct Scene {
     HostTree T;
     LeafClusters C;
     std::vector<float> sph;  // per slot: bounding sphere centre + radius (f32, exact enough for a model)
+    std::vector<int32_t> rank;          // leaf node -> static discovery rank (inner_table)
+    std::vector<int32_t> rlo, rhi;      // node -> smallest / largest leaf rank below it
 };
+
+struct Walk { double rays = 0, ref_visits = 0, lazy_visits = 0, lazy_pq_visits = 0, k8_visits = 0, lr_visits = 0, lr_passes = 0, k8_passes = 0; };
+Walk g_walk[3];
+int g_level = 0;
+int g_min_safe = 1;  // lazy_restart: safe leaves a pass returns at least (argv[4])
+
+// Inner-node visits of three traversal schedules for the same query (the leaf set and order are the
+// reference's; only the visiting differs):
+//   ref   the reference DFS (every discovered node examined);
+//   k8    near-first passes into an 8-leaf buffer with subtree skipping once full, re-walks after
+//         the buffer's last leaf (the kernel's traverse_pass_near);
+//   lazy  near-first DFS that scans a leaf as soon as no pending subtree can hold a leaf before it
+//         in (distance, rank) order, and stops at the leaf that ends the query; lazy_pq the same
+//         with the pending subtrees in a priority queue (a lower bound).
+void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std::pair<float, int>>& ref_leaves);
 
 // One query with the kernel's clustered scan; returns best t (kMaxFloat none) and the hit slot.
 float trace(const Scene& S, V3 o, V3 d, Cls* cls, uint32_t& hit_slot) {
@@ -123,6 +140,7 @@ float trace(const Scene& S, V3 o, V3 d, Cls* cls, uint32_t& hit_slot) {
     }
     float best = kMaxFloat;
     bool first_leaf = true;
+    int improving = -1;  // node id of the leaf that ended the query (-1: none)
     for (auto& lf : leaves) {
         if (cls) cls->leaves += 1;
         const uint32_t c0 = C.range[2 * size_t(lf.second)], nc = C.range[2 * size_t(lf.second) + 1];
@@ -192,9 +210,208 @@ float trace(const Scene& S, V3 o, V3 d, Cls* cls, uint32_t& hit_slot) {
             }
         }
         first_leaf = false;
-        if (improved) break;
+        if (improved) { improving = lf.second; break; }
     }
+    if (cls) walk_model(S, o, d, improving, leaves);
     return best;
+}
+
+struct Pend { float bound; int32_t rlo; int32_t node; };
+bool lex_less(float d, int32_t r, float d2, int32_t r2) { return d < d2 || (d == d2 && r < r2); }
+
+// near-first child order: children in the ray's crossing order (index mirrored by the direction's
+// signs, as traverse_pass_near), examined with the reference's first-5-hits rule in child order.
+struct Examined { std::vector<std::pair<float, int32_t>> leaves; std::vector<Pend> inner; };
+Examined examine(const Scene& S, V3 o, V3 inv, int32_t node) {
+    const HostTree& T = S.T;
+    Examined e;
+    const int32_t ch = T.children[size_t(node)];
+    int hit = 0;
+    bool hitv[8] = {};
+    for (int i = 0; i < 8 && hit <= 4; ++i) {
+        const int32_t c = ch + i;
+        const float* b = &T.bounds[6 * size_t(c)];
+        if (T.children[size_t(c)]) {
+            if (box_check(o, inv, b)) { ++hit; hitv[i] = true; }
+        } else {
+            const float dis = box_entry(o, inv, b);
+            if (dis > 0) { ++hit; hitv[i] = true; }
+        }
+    }
+    const int sm = (inv.x < 0) * 4 + (inv.y < 0) * 2 + (inv.z < 0);
+    for (int k = 0; k < 8; ++k) {
+        const int i = k ^ sm;
+        if (!hitv[i]) continue;
+        const int32_t c = ch + i;
+        const float* b = &T.bounds[6 * size_t(c)];
+        if (T.children[size_t(c)]) {
+            // lower bound of the leaf distances below: the box entry if in front, else 0
+            const int s0 = inv.x < 0, s1 = inv.y < 0, s2 = inv.z < 0;
+            float tmin = ((s0 ? b[3] : b[0]) - o.x) * inv.x;
+            tmin = std::max(tmin, ((s1 ? b[4] : b[1]) - o.y) * inv.y);
+            tmin = std::max(tmin, ((s2 ? b[5] : b[2]) - o.z) * inv.z);
+            float tmax = ((s0 ? b[0] : b[3]) - o.x) * inv.x;
+            tmax = std::min(tmax, ((s1 ? b[1] : b[4]) - o.y) * inv.y);
+            tmax = std::min(tmax, ((s2 ? b[2] : b[5]) - o.z) * inv.z);
+            if (tmax <= 0) continue;  // nothing in front
+            e.inner.push_back({std::max(tmin, 0.f), S.rlo[size_t(c)], c});
+        } else {
+            e.leaves.push_back({box_entry(o, inv, b), S.rank[size_t(c)]});
+        }
+    }
+    return e;
+}
+
+void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std::pair<float, int>>& ref_leaves) {
+    const HostTree& T = S.T;
+    Walk& W = g_walk[g_level];
+    W.rays += 1;
+    const V3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+    if (!box_check(o, inv, &T.bounds[0]) || T.children[0] == 0) return;
+    const int32_t stop_rank = improving >= 0 ? S.rank[size_t(improving)] : -1;
+    // ref: every inner node the reference DFS examines
+    {
+        std::vector<int32_t> st(1, 0);
+        while (!st.empty()) {
+            const int32_t cur = st.back();
+            st.pop_back();
+            W.ref_visits += 1;
+            const int32_t ch = T.children[size_t(cur)];
+            int hit = 0;
+            for (int i = 0; i < 8 && hit <= 4; ++i) {
+                const int32_t c = ch + i;
+                if (T.children[size_t(c)]) {
+                    if (box_check(o, inv, &T.bounds[6 * size_t(c)])) { ++hit; st.push_back(c); }
+                } else if (box_entry(o, inv, &T.bounds[6 * size_t(c)]) > 0) ++hit;
+            }
+        }
+    }
+    // lazy (DFS stack order) and lazy_pq (priority queue)
+    for (int pq = 0; pq < 2; ++pq) {
+        std::vector<Pend> pend{{0.f, S.rlo[0], 0}};
+        std::vector<std::pair<float, int32_t>> found;  // sorted (dist, rank)
+        double visits = 0;
+        bool done = false;
+        while (!done) {
+            // scan every safe leaf
+            while (!found.empty()) {
+                bool safe = true;
+                for (const Pend& p : pend)
+                    if (!lex_less(found[0].first, found[0].second, p.bound, p.rlo)) { safe = false; break; }
+                if (!safe) break;
+                if (found[0].second == stop_rank) { done = true; break; }
+                found.erase(found.begin());
+            }
+            if (done || pend.empty()) break;
+            size_t pick = pend.size() - 1;
+            if (pq)
+                for (size_t i = 0; i < pend.size(); ++i)
+                    if (lex_less(pend[i].bound, pend[i].rlo, pend[pick].bound, pend[pick].rlo)) pick = i;
+            const Pend p = pend[pick];
+            pend.erase(pend.begin() + long(pick));
+            visits += 1;
+            Examined e = examine(S, o, inv, p.node);
+            for (auto& lf : e.leaves) {
+                auto it = std::lower_bound(found.begin(), found.end(), lf, [](const std::pair<float, int32_t>& a,
+                                                                               const std::pair<float, int32_t>& b) {
+                    return lex_less(a.first, a.second, b.first, b.second);
+                });
+                found.insert(it, lf);
+            }
+            // DFS order: push the far children first so the nearest is on top
+            for (auto it = e.inner.rbegin(); it != e.inner.rend(); ++it) pend.push_back(*it);
+        }
+        (pq ? W.lazy_pq_visits : W.lazy_visits) += visits;
+    }
+    // lazy_restart: near-first passes that return as soon as some found leaf is safe (every safe leaf,
+    // at most K), the leaves scanned, then a re-walk from the root after the last returned leaf
+    // (no traversal state kept across the leaf scans); inner children whose exit is at or before
+    // the re-walk bound are not entered (the kernel's cull rule)
+    {
+        const int K = 8;
+        float bd = -1e30f;
+        int32_t bi = -1;
+        double visits = 0, passes = 0;
+        for (;;) {
+            passes += 1;
+            std::vector<Pend> pend{{0.f, S.rlo[0], 0}};
+            std::vector<std::pair<float, int32_t>> found;
+            std::vector<std::pair<float, int32_t>> out;
+            for (;;) {
+                while (!found.empty() && (int)out.size() < K) {
+                    bool safe = true;
+                    for (const Pend& p : pend)
+                        if (!lex_less(found[0].first, found[0].second, p.bound, p.rlo)) { safe = false; break; }
+                    if (!safe) break;
+                    out.push_back(found[0]);
+                    found.erase(found.begin());
+                }
+                if ((int)out.size() >= g_min_safe || pend.empty()) break;
+                const Pend p = pend.back();
+                pend.pop_back();
+                visits += 1;
+                Examined e = examine(S, o, inv, p.node);
+                for (auto& lf : e.leaves) {
+                    if (!lex_less(bd, bi, lf.first, lf.second)) continue;
+                    auto it = std::lower_bound(found.begin(), found.end(), lf, [](const std::pair<float, int32_t>& a,
+                                                                               const std::pair<float, int32_t>& b) {
+                        return lex_less(a.first, a.second, b.first, b.second);
+                    });
+                    found.insert(it, lf);
+                }
+                for (auto it = e.inner.rbegin(); it != e.inner.rend(); ++it) pend.push_back(*it);
+            }
+            bool stop = out.empty();
+            for (auto& lf : out)
+                if (lf.second == stop_rank) stop = true;
+            if (stop) break;
+            bd = out.back().first;
+            bi = out.back().second;
+        }
+        W.lr_visits += visits;
+        W.lr_passes += passes;
+    }
+    // k8: near-first passes with an 8-leaf buffer, subtree skip when full, re-walk after the buffer
+    {
+        const int K = 8;
+        float bd = -1e30f;
+        int32_t bi = -1;
+        double visits = 0;
+        for (;;) {
+            W.k8_passes += 1;
+            std::vector<std::pair<float, int32_t>> buf;  // sorted, at most K
+            bool more = false;
+            std::vector<Pend> st{{0.f, S.rlo[0], 0}};
+            while (!st.empty()) {
+                const Pend p = st.back();
+                st.pop_back();
+                if ((int)buf.size() == K && !lex_less(p.bound, p.rlo, buf.back().first, buf.back().second)) {
+                    more = true;
+                    continue;
+                }
+                visits += 1;
+                Examined e = examine(S, o, inv, p.node);
+                for (auto& lf : e.leaves) {
+                    if (!lex_less(bd, bi, lf.first, lf.second)) continue;  // at or before the re-walk bound
+                    auto it = std::lower_bound(buf.begin(), buf.end(), lf, [](const std::pair<float, int32_t>& a,
+                                                                             const std::pair<float, int32_t>& b) {
+                        return lex_less(a.first, a.second, b.first, b.second);
+                    });
+                    buf.insert(it, lf);
+                    if ((int)buf.size() > K) { buf.pop_back(); more = true; }
+                }
+                for (auto it = e.inner.rbegin(); it != e.inner.rend(); ++it) st.push_back(*it);
+            }
+            bool stop = false;
+            for (auto& lf : buf)
+                if (lf.second == stop_rank) { stop = true; break; }
+            if (stop || !more || buf.empty()) break;
+            bd = buf.back().first;
+            bi = buf.back().second;
+        }
+        W.k8_visits += visits;
+    }
+    (void)ref_leaves;
 }
 
 }  // namespace
@@ -203,6 +420,7 @@ int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: bounce_sim OBJ [step] [spp]\n"); return 2; }
     const int step = argc > 2 ? std::atoi(argv[2]) : 8;
     const int spp = argc > 3 ? std::atoi(argv[3]) : 4;
+    if (argc > 4) g_min_safe = std::atoi(argv[4]);
     std::ifstream f(argv[1], std::ios::binary);
     std::stringstream ss;
     ss << f.rdbuf();
@@ -215,6 +433,21 @@ int main(int argc, char** argv) {
     Scene S;
     if (octree_build(M, 300, S.T)) return 1;
     if (leaf_clusters(S.T, 16, S.C)) return 1;
+    {
+        std::vector<float4_t> inner;
+        if (inner_table(S.T, inner, S.rank)) return 1;
+        const int32_t nn = S.T.nnodes;
+        S.rlo.assign(size_t(nn), 1 << 30);
+        S.rhi.assign(size_t(nn), -1);
+        for (int32_t n = nn - 1; n >= 0; --n) {  // children come after their parent in node order
+            if (S.T.children[size_t(n)] == 0) { S.rlo[size_t(n)] = S.rhi[size_t(n)] = S.rank[size_t(n)]; continue; }
+            for (int i = 0; i < 8; ++i) {
+                const int32_t c = S.T.children[size_t(n)] + i;
+                S.rlo[size_t(n)] = std::min(S.rlo[size_t(n)], S.rlo[size_t(c)]);
+                S.rhi[size_t(n)] = std::max(S.rhi[size_t(n)], S.rhi[size_t(c)]);
+            }
+        }
+    }
     const size_t nslots = S.C.order.size();
     S.sph.resize(4 * nslots);
     for (size_t k = 0; k < nslots; ++k) {
@@ -239,6 +472,7 @@ int main(int argc, char** argv) {
             const float film_x = ((-1.0f + 2.0f * (float(x) / float(cm.width))) * cm.h_fov) * cm.aspect_ratio;
             const V3 d0 = unit(sub(add(add(fc, scale(cx, film_x)), scale(cy, film_y)), eye));
             uint32_t slot;
+            g_level = 0;
             const float t0 = trace(S, eye, d0, &cam, slot);
             if (slot == 0xFFFFFFFFu) continue;
             for (int s = 0; s < spp; ++s) {
@@ -252,6 +486,7 @@ int main(int argc, char** argv) {
                     const V3 rnd = unit(add(mk(rbi(st), rbi(st), rbi(st)), n));
                     const V3 pure = unit(sub(d, scale(n, 2 * dot(d, n))));
                     d = unit(add(scale(rnd, 0.7f), scale(pure, 0.3f)));  // lerp(rnd, pure, 0.3)
+                    g_level = level;
                     const float t = trace(S, o, d, level == 1 ? &b1 : &b2, sl);
                     if (sl == 0xFFFFFFFFu) break;
                     o = add(o, scale(d, t));
@@ -267,6 +502,13 @@ int main(int argc, char** argv) {
                     c.far / a, c.uv / a, c.culled / a, c.origin_leaf_full / a, c.plane_keep / a, c.sphere_keep / a,
                     c.both_keep / a);
     };
+    for (int l = 0; l < 3; ++l) {
+        const Walk& w = g_walk[l];
+        std::printf("level %d inner-node visits per ray: reference %.2f  k8 passes %.2f (%.2f passes)  lazy %.2f  lazy (priority) %.2f"
+                    "  lazy with restarts %.2f (%.2f passes)\n",
+                    l, w.ref_visits / w.rays, w.k8_visits / w.rays, w.k8_passes / w.rays, w.lazy_visits / w.rays,
+                    w.lazy_pq_visits / w.rays, w.lr_visits / w.rays, w.lr_passes / w.rays);
+    }
     pr("camera", cam);
     pr("bounce1", b1);
     pr("bounce2", b2);
