@@ -131,12 +131,30 @@ __device__ __forceinline__ TriRec load_tri(const DTri* __restrict__ tris, uint32
     return t;
 }
 
+// 1 / x correctly rounded (the reference's f32 division, model.h:84) for the culled test's det
+// (x >= kTol): the hardware reciprocal (1 ulp) and two FMA corrections, 5 VALU instead of the
+// 10 of the general IEEE division expansion (scaling, denormal and overflow handling the det never
+// needs). Checked equal to 1.0f / x bit for bit for every f32 in [2^-14, 2^64) on the GPU
+// (tests/c/recip_check.hip, tests/test_gpu_recip.py); outside that range (and for NaN) the division.
+__device__ __forceinline__ float recip_det(float x) {
+#ifdef ATR_IEEE_RECIP
+    return 1.0f / x;
+#else
+    if (!(x < 18446744073709551616.0f)) return 1.0f / x;  // 2^64
+    float r = __builtin_amdgcn_rcpf(x);
+    float e = __builtin_fmaf(-x, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+#endif
+}
+
 // get_triangle_ray_intersection_culled (model.h:75-103); ab/ac precomputed on the host.
 __device__ __forceinline__ float tri_hit(const Ray& r, V3 a, V3 ab, V3 ac, float& u, float& v) {
     const V3 pvec = cross(r.d, ac);
     const float det = dot(ab, pvec);
     if (det < kTol) return 0;
-    const float det_inv = 1 / det;
+    const float det_inv = recip_det(det);
     const V3 tvec = sub(r.o, a);
     u = dot(tvec, pvec) * det_inv;
     if (u < 0 || u > 1) return 0;
