@@ -922,7 +922,7 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
         t->path_batch_log2 < 12 || t->path_batch_log2 > 28 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
         t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
         (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)) ||
-        (t->primary_occ != 0 && t->primary_occ != 6 && t->primary_occ != 7))
+        (t->primary_occ != 0 && (t->primary_occ < 6 || t->primary_occ > 8)))
         return ATR_E_INVALID;
     for (int32_t r : t->reserved)
         if (r) return ATR_E_INVALID;

@@ -278,6 +278,7 @@ template __global__ void render_kernel<SCHED_LANE, true, true>(RenderParams);
 template __global__ void render_kernel<SCHED_LANE, false, true, 5>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 6>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, true, 7>(RenderParams);
+template __global__ void render_kernel<SCHED_HYBRID, false, true, 8>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, false, false>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, true, true>(RenderParams);
 template __global__ void render_kernel<SCHED_HYBRID, true, false>(RenderParams);
@@ -373,11 +374,13 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, i
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing && P.cam.samples_per_pixel == 1;
     const bool multi = P.frame_blocks > 0;
-    const bool prim7 = primary_occ ? primary_occ == 7 : multi;
+    const bool prim7 = primary_occ ? primary_occ >= 7 : multi;
+    const bool prim8 = primary_occ == 8;
     switch (sched) {
         case SCHED_HYBRID:
             if (count) { if (prim) launch_one<SCHED_HYBRID, true, true>(P, s); else launch_one<SCHED_HYBRID, true, false>(P, s); }
             else if (!prim) launch_one<SCHED_HYBRID, false, false>(P, s);  // LDS: 4 workgroups per CU
+            else if (prim8) launch_one<SCHED_HYBRID, false, true, 8>(P, s);
             else if (prim7) launch_one<SCHED_HYBRID, false, true, 7>(P, s);
             else launch_one<SCHED_HYBRID, false, true, 6>(P, s);
             break;

@@ -156,18 +156,25 @@ __device__ __forceinline__ int32_t wave_incl_max(int32_t x) {
 
 // LDS of the FLAT/HYBRID scans (22.5 KB per 4-wave workgroup): the leaf order buffers (lane-private
 // columns), the per-owner best keys and hit records, the round's owner markers.
-template <int K = kLeafBuf>
-struct FlatLds {
+// The hit's barycentrics per owner (an empty base when no output needs them: the primary-only
+// kernels' LDS is then 20 KB per workgroup, so 8 of them fit a CU's 160 KB).
+template <bool UV>
+struct FlatUV {
+    float u[4][64], v[4][64];
+};
+template <>
+struct FlatUV<false> {};
+template <int K = kLeafBuf, bool UV = true>
+struct FlatLds : FlatUV<UV> {
     float lbd[4][K][64];
     int32_t lbl[4][K][64];
     unsigned long long key[4][64];
     uint32_t slot[4][64];
-    float u[4][64], v[4][64];
     int32_t mark[4][64];
 };
-template <int K = kLeafBuf>
-__device__ __forceinline__ FlatLds<K>& flat_lds() {
-    __shared__ FlatLds<K> L;
+template <int K = kLeafBuf, bool UV = true>
+__device__ __forceinline__ FlatLds<K, UV>& flat_lds() {
+    __shared__ FlatLds<K, UV> L;
     return L;
 }
 
@@ -176,10 +183,10 @@ constexpr unsigned long long kKeyInit = (static_cast<unsigned long long>(0x7F7FF
 // One full test of candidate `slot` for the ray q of owner lane `ow`: lowers the owner's (t bits,
 // leaf rank) key in LDS -- the minimum over the leaf in any order is the reference's
 // first-in-leaf-order closest hit (kd_tree.cpp:440-456); true if this test lowered it.
-template <bool COUNT, int K = kLeafBuf>
+template <bool COUNT, int K = kLeafBuf, bool UV = true>
 __device__ __forceinline__ bool cand_test(const Ray& q, const DModel& m, int w, int32_t ow, uint32_t slot,
                                           unsigned long long& mine, float& u, float& v, Ctr& ct) {
-    FlatLds<K>& L = flat_lds<K>();
+    FlatLds<K, UV>& L = flat_lds<K, UV>();
     if constexpr (COUNT) ct.tri += 1;
     float4_t a0, a1, a2;
     load_prim(m, slot, a0, a1, a2);
@@ -209,7 +216,7 @@ __device__ __forceinline__ bool cand_test(const Ray& q, const DModel& m, int w, 
 template <bool COUNT, bool UO, bool NUV, bool SELF = false, int K = kLeafBuf>
 __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w, int ln, uint32_t cm,
                                             uint32_t cfirst, int32_t own, Ctr& ct) {
-    FlatLds<K>& L = flat_lds<K>();
+    FlatLds<K, !NUV>& L = flat_lds<K, !NUV>();
     const uint32_t cc = uint32_t(__popc(cm));
     constexpr bool kInPlace = SELF;
 #ifndef ATR_INPLACE_FACTOR
@@ -242,7 +249,7 @@ __device__ __forceinline__ void cand_rounds(const Ray& r, const DModel& m, int w
             unsigned long long mine = kKeyInit;
             bool imp = false;
             float u = 0.f, v = 0.f;
-            if (valid) imp = cand_test<COUNT, K>(q, m, w, own, slot, mine, u, v, ct);
+            if (valid) imp = cand_test<COUNT, K, !NUV>(q, m, w, own, slot, mine, u, v, ct);
             __builtin_amdgcn_wave_barrier();
             if (imp && L.key[w][own] == mine) {  // this iteration's winner for its owner
                 L.slot[w][own] = slot;
@@ -324,9 +331,9 @@ struct FlatQ {
     bool done, need, more, rewalk;
 };
 
-template <bool COUNT, int K = kLeafBuf>
+template <bool COUNT, int K = kLeafBuf, bool UV = true>
 __device__ __forceinline__ FlatQ flat_begin(const Ray& r, const DModel& m, bool active, int w, int ln, Ctr& ct) {
-    FlatLds<K>& L = flat_lds<K>();
+    FlatLds<K, UV>& L = flat_lds<K, UV>();
     FlatQ q{0, 0, true, false, false, false};
     L.key[w][ln] = kKeyInit;
     if (active) {
@@ -349,9 +356,9 @@ __device__ __forceinline__ FlatQ flat_begin(const Ray& r, const DModel& m, bool 
 // One DFS pass (kd_tree.cpp:363-435) for every lane with `need`; its sorted leaves wait in LDS.
 // UT: the wave walks its passes together (traverse_pass_wave: coherent rays). LDSB: the pass inserts
 // straight into the LDS columns. NEAR (with LDSB): near-first passes (traverse_pass_near).
-template <bool COUNT, bool LDSB, bool UT, bool NEAR, int K = kLeafBuf>
+template <bool COUNT, bool LDSB, bool UT, bool NEAR, int K = kLeafBuf, bool UV = true>
 __device__ __forceinline__ void flat_pass(const Ray& r, const DModel& m, int w, int ln, FlatQ& q, int& err, Ctr& ct) {
-    FlatLds<K>& L = flat_lds<K>();
+    FlatLds<K, UV>& L = flat_lds<K, UV>();
     // the re-walk bound: the last leaf of the previous pass's full buffer (entry K - 1 of the column)
     const float bd = q.rewalk ? L.lbd[w][K - 1][ln] : -__builtin_inff();
     const int32_t bi = q.rewalk ? L.lbl[w][K - 1][ln] : -1;
@@ -397,7 +404,7 @@ __device__ __forceinline__ void flat_pass(const Ray& r, const DModel& m, int w, 
 template <bool COUNT, bool HYB, bool UO, bool NUV, int K = kLeafBuf>
 __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, int w, int ln, bool live, FlatQ& q,
                                                Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
-    FlatLds<K>& L = flat_lds<K>();
+    FlatLds<K, !NUV>& L = flat_lds<K, !NUV>();
     ATR_PCLK(const uint64_t tc2 = clock64());
     uint32_t cf = 0, cn = 0;
     if (live) {
@@ -477,7 +484,7 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
 // The lane's result from its LDS row (t = kMaxFloat: no hit).
 template <bool NUV, int K = kLeafBuf>
 __device__ __forceinline__ void flat_result(const DModel& m, bool active, int w, int ln, Hit& h) {
-    FlatLds<K>& L = flat_lds<K>();
+    FlatLds<K, !NUV>& L = flat_lds<K, !NUV>();
     h.t = kMaxFloat;
     h.face = 0;
     h.u = h.v = 0.f;
@@ -500,10 +507,10 @@ __device__ __forceinline__ void tree_closest_flat(const Ray& r, const DModel& m,
                                                   Ctr& ct, int32_t hyb_a = 0, int32_t hyb_b = 0) {
     const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
     ATR_PCLK(uint64_t tcs = clock64());
-    FlatQ q = flat_begin<COUNT, K>(r, m, active, w, ln, ct);
+    FlatQ q = flat_begin<COUNT, K, !NUV>(r, m, active, w, ln, ct);
     for (;;) {
         ATR_PCLK(const uint64_t tc0 = clock64());
-        flat_pass<COUNT, LDSB, UT, NEAR, K>(r, m, w, ln, q, err, ct);
+        flat_pass<COUNT, LDSB, UT, NEAR, K, !NUV>(r, m, w, ln, q, err, ct);
         ATR_PCLK(ct.t_pass += uint32_t(clock64() - tc0));
         if (__ballot(!q.done) == 0) break;
         flat_leaf_step<COUNT, HYB, UO, NUV, K>(r, m, w, ln, !q.done, q, ct, hyb_a, hyb_b);
