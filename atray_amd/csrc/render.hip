@@ -365,8 +365,8 @@ static void launch_one(const atr::RenderParams& P, hipStream_t s) {
 }
 
 // sched: 0 LANE, 6 FLAT, 7 HYBRID (capi.cpp sched_of). Occupancy per schedule and launch shape by
-// measurement: one frame at 6 waves/SIMD (its slowest cells set the latency),
-// frames in flight at 7 (throughput); primary_occ 6 / 7 overrides the HYBRID primary choice.
+// measurement: HYBRID primaries one frame at 8 waves/SIMD, frames in flight at 7;
+// primary_occ 6 / 7 / 8 overrides the choice.
 extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, int primary_occ, hipStream_t s) {
     using namespace atr;
     if (P.nblocks <= 0) return hipSuccess;
@@ -374,8 +374,11 @@ extern "C" hipError_t atr_launch_render(const atr::RenderParams& P, int sched, i
     const bool count = P.counters != nullptr;
     const bool prim = P.cam.bounce_limit == 1 && !P.cam.anti_aliasing && P.cam.samples_per_pixel == 1;
     const bool multi = P.frame_blocks > 0;
-    const bool prim7 = primary_occ ? primary_occ >= 7 : multi;
-    const bool prim8 = primary_occ == 8;
+    // default: frames in flight at 7 waves/SIMD, one frame at 8 (one frame alone 0.333 vs 0.345 ms
+    // at 6 waves; frames in flight equal at 7 and 8)
+    const int occ = primary_occ ? primary_occ : (multi ? 7 : 8);
+    const bool prim7 = occ == 7;
+    const bool prim8 = occ == 8;
     switch (sched) {
         case SCHED_HYBRID:
             if (count) { if (prim) launch_one<SCHED_HYBRID, true, true>(P, s); else launch_one<SCHED_HYBRID, true, false>(P, s); }

@@ -175,8 +175,9 @@ typedef struct {
                                block list */
     int32_t path_camera_occ; /* PATHS: waves/SIMD of the camera-ray and bounce launches, 5..7, */
     int32_t path_bounce_occ; /* or 0 = the measured default */
-    int32_t primary_occ;    /* HYBRID primary cell launches: waves/SIMD 6 or 7, or 0 = the measured
-                               default (6 for one frame, 7 for frames in flight) */
+    int32_t primary_occ;    /* HYBRID primary cell launches: waves/SIMD 6, 7 or 8, or 0 = the
+                               measured default (8 for one frame, 7 for frames in flight;
+                               DESIGN.md §4e) */
     int32_t reserved[2];    /* must be 0 */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
