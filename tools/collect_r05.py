@@ -1,8 +1,15 @@
-"""Collect round-5 shard sets into profiles/r05/sim_shards.json: for each config the full-frame
-line and every rank of the N-way plans (bench.py --sim-world N --sim-rank r) found in a gpurun_out
-directory (files <cfg>_full.json, <cfg>_sim<N>_r<r>.json, as tools/gpu_r5_a.sh / gpu_r5_sim.sh
-write them). Usage: python tools/collect_r05.py gpurun_out/r5a [more dirs ...]; then
-tools/project_n.py turns the file into the 1/2/4/8 projection."""
+"""Collect round-5 measurement sets into profiles/r05/.
+
+  python tools/collect_r05.py sim gpurun_out/r5a [more dirs ...]
+      shard sets -> profiles/r05/sim_shards.json: for each config the full-frame line and every
+      rank of the N-way plans (bench.py --sim-world N --sim-rank r) found in the directories (files
+      <cfg>_full.json, <cfg>_sim<N>_r<r>.json, as tools/gpu_r5_a.sh / gpu_r5_sim.sh write them);
+      tools/project_n.py turns the file into the 1/2/4/8 projection.
+  python tools/collect_r05.py final gpurun_out/r5final
+      the bench lines (bench_<cfg>.json), their PMC rows (gpurun_out/bench_pmc/rows_<cfg>.json, named
+      after the kernel and grid / dispatch count), verify_r05.json (traffic, VALU and L2 hit rate
+      recomputed from the rows, must agree with the lines within 1 %), the GPU suite and smoke
+      tails, and the rocprofv3 kernel traces' stats and summaries (tools/trace_summary.py)."""
 import glob
 import json
 import os
@@ -19,35 +26,113 @@ def last_json(path):
     return json.loads(lines[-1])
 
 
-out_path = os.path.join(P, "sim_shards.json")
-sim = json.load(open(out_path)) if os.path.exists(out_path) else {}
-for d in sys.argv[1:]:
-    for full_path in sorted(glob.glob(os.path.join(d, "*_full.json"))):
-        cfg = os.path.basename(full_path).split("_")[0]
-        full = last_json(full_path)
-        worlds = sorted({int(m.group(1)) for f in glob.glob(os.path.join(d, f"{cfg}_sim*_r*.json"))
-                         for m in [re.search(r"_sim(\d+)_r\d+\.json$", f)] if m})
-        for N in worlds:
-            ranks = []
-            for r in range(N):
-                f = os.path.join(d, f"{cfg}_sim{N}_r{r}.json")
-                if not os.path.exists(f):
-                    break
-                x = last_json(f)
-                ranks.append({"rank": r, "ms_per_frame": x["ms_per_step"], "mrays_s": x["value"],
-                              "single_frame_latency_ms": x["single_frame"].get("latency_ms"),
-                              "launches": x["config"].get("launches"),
-                              "launch_render_done_ms": x["config"].get("launch_render_done_ms")})
-            if len(ranks) != N:
-                continue
-            mx = max(x["ms_per_frame"] for x in ranks)
-            sim.setdefault(cfg, {})[str(N)] = {
-                "source": os.path.relpath(d, R), "workload": full["config"]["workload"],
-                "shape": {"launches": ranks[0]["launches"] or full["config"]["launches"],
-                          "streams": full["config"]["streams"]},
-                "full_frame": {"ms_per_frame": full["ms_per_step"], "mrays_s": full["value"],
-                               "single_frame_latency_ms": full["single_frame"].get("latency_ms")},
-                "ranks": ranks, "max_shard_ms_per_frame": mx,
-                "render_side_speedup": round(full["ms_per_step"] / mx, 3)}
-            print(cfg, N, sim[cfg][str(N)]["render_side_speedup"], mx, full["ms_per_step"])
-json.dump(sim, open(out_path, "w"), indent=1)
+def collect_sim(dirs):
+    out_path = os.path.join(P, "sim_shards.json")
+    sim = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    for d in dirs:
+        for full_path in sorted(glob.glob(os.path.join(d, "*_full.json"))):
+            cfg = os.path.basename(full_path).split("_")[0]
+            full = last_json(full_path)
+            worlds = sorted({int(m.group(1)) for f in glob.glob(os.path.join(d, f"{cfg}_sim*_r*.json"))
+                             for m in [re.search(r"_sim(\d+)_r\d+\.json$", f)] if m})
+            for N in worlds:
+                ranks = []
+                for r in range(N):
+                    f = os.path.join(d, f"{cfg}_sim{N}_r{r}.json")
+                    if not os.path.exists(f):
+                        break
+                    x = last_json(f)
+                    ranks.append({"rank": r, "ms_per_frame": x["ms_per_step"], "mrays_s": x["value"],
+                                  "single_frame_latency_ms": x["single_frame"].get("latency_ms"),
+                                  "launches": x["config"].get("launches"),
+                                  "launch_render_done_ms": x["config"].get("launch_render_done_ms")})
+                if len(ranks) != N:
+                    continue
+                mx = max(x["ms_per_frame"] for x in ranks)
+                sim.setdefault(cfg, {})[str(N)] = {
+                    "source": os.path.relpath(d, R), "workload": full["config"]["workload"],
+                    "shape": {"launches": ranks[0]["launches"] or full["config"]["launches"],
+                              "streams": full["config"]["streams"]},
+                    "full_frame": {"ms_per_frame": full["ms_per_step"], "mrays_s": full["value"],
+                                   "single_frame_latency_ms": full["single_frame"].get("latency_ms")},
+                    "ranks": ranks, "max_shard_ms_per_frame": mx,
+                    "render_side_speedup": round(full["ms_per_step"] / mx, 3)}
+                print(cfg, N, sim[cfg][str(N)]["render_side_speedup"], mx, full["ms_per_step"])
+    json.dump(sim, open(out_path, "w"), indent=1)
+
+
+def kernel_tag(name):
+    """'void atr::render_kernel<7, false, true, 7>(...)' -> 'render_kernel_7_false_true_7'."""
+    base = name.split("(")[0].replace("void ", "").replace("atr::", "")
+    return re.sub(r"[^A-Za-z0-9]+", "_", base).strip("_")
+
+
+def collect_final(d):
+    import collections
+    import shutil
+    import subprocess
+    G = os.path.join(R, "gpurun_out")
+    verify = {}
+    for cfg in ("c3", "c4", "c5"):
+        src = os.path.join(d, f"bench_{cfg}.json")
+        if not os.path.exists(src):
+            continue
+        line = last_json(src)
+        json.dump(line, open(f"{P}/bench_{cfg}.json", "w"), indent=1)
+        rows_path = f"{G}/bench_pmc/rows_{cfg}.json"
+        if not os.path.exists(rows_path):
+            continue
+        rows = json.load(open(rows_path))
+        sel = rows["selection"]
+        kernels = sorted({r[0] for r in rows["rows"]})
+        if sel == "largest grid":
+            name = f"pmc_{cfg}_{kernel_tag(kernels[0])}_grid{rows['rows'][0][1]}.json"
+        else:
+            name = f"pmc_{cfg}_path_kernels_{sum(sel['last dispatches'].values())}_timed_dispatches.json"
+        json.dump(rows, open(f"{P}/{name}", "w"))
+        tot, cnt = collections.defaultdict(float), collections.defaultdict(int)
+        for _, _, _, c, v in rows["rows"]:
+            tot[c] += v
+            cnt[c] += 1
+        roof = line["roofline"]
+        if sel == "largest grid":
+            fpl = max(roof["frames_per_launch"])
+            mean = {c: tot[c] / cnt[c] for c in tot}
+            traffic_frame = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0 / fpl
+            valu_frame = mean.get("SQ_INSTS_VALU", 0.0) / fpl
+        else:
+            traffic_frame = (2.0 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0 / line["steps"]
+            valu_frame = tot.get("SQ_INSTS_VALU", 0.0) / line["steps"]
+        hit = tot.get("TCC_HIT_sum", 0.0) / max(1.0, tot.get("TCC_HIT_sum", 0.0) + tot.get("TCC_MISS_sum", 0.0))
+        got = {"traffic_per_frame": traffic_frame, "valu_wave_insts_per_frame": valu_frame, "l2_hit_rate": hit}
+        want = {"traffic_per_frame": roof.get("traffic_per_frame"),
+                "valu_wave_insts_per_frame": (roof.get("valu") or {}).get("wave_insts_per_frame"),
+                "l2_hit_rate": roof.get("l2_hit_rate")}
+        verify[cfg] = {"file": name, "recomputed": got, "bench_line": want,
+                       "agree_1pct": all(w is None or abs(g - w) <= 0.01 * abs(w) for g, w in
+                                         ((got[k], want[k]) for k in got))}
+        print(cfg, name, verify[cfg]["agree_1pct"])
+    if verify:
+        json.dump(verify, open(f"{P}/verify_r05.json", "w"), indent=1)
+    for f in ("pytest_gpu.log", "smoke.log"):
+        if os.path.exists(f"{d}/{f}"):
+            lines = open(f"{d}/{f}").read().strip().splitlines()
+            open(f"{P}/{f.replace('.log', '_tail.txt')}", "w").write("\n".join(lines[-3:]) + "\n")
+    fpl = {"trace_c3_driver": 10, "trace_c4": 4}  # frames per timed launch of the traced command
+    for t in glob.glob(f"{d}/trace_*"):
+        if os.path.isdir(t):
+            tag = os.path.basename(t)
+            for f in glob.glob(f"{t}/**/*kernel_stats.csv", recursive=True):
+                shutil.copy(f, f"{P}/{tag}_kernel_stats.csv")
+            with open(f"{P}/{tag}_summary.json", "w") as fh:
+                subprocess.run([sys.executable, f"{R}/tools/trace_summary.py", t, str(fpl.get(tag, 4)),
+                                f"{P}/{tag}_kernel_stats.csv"], stdout=fh, check=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "sim":
+        collect_sim(sys.argv[2:])
+    elif sys.argv[1] == "final":
+        collect_final(sys.argv[2])
+    else:
+        sys.exit(__doc__)
