@@ -98,6 +98,7 @@ int main(int argc, char** argv) {
         return box_check(o, inv, bb) && !(box_entry(o, inv, bb) > best);
     };
     double iters_now = 0, iters_super = 0, leaf_steps = 0, union_clusters = 0;
+    std::vector<std::pair<int, int>> cell_steps;  // per cell: wave leaf steps now / with tail speculation
     std::vector<std::pair<float, int>> leaves;
     std::vector<int32_t> stack;
     const int cw = (cm.width + 7) / 8, chh = (cm.height + 7) / 8;
@@ -105,6 +106,7 @@ int main(int argc, char** argv) {
         for (int cxi = 0; cxi < cw; ++cxi) {
             // per leaf scanned by any ray of the cell: which clusters some ray passes
             std::map<int, std::vector<char>> used;
+            std::vector<int> nleaves;  // per active ray: leaves scanned (the query's leaf steps)
             for (int ly = 0; ly < 8; ++ly)
                 for (int lx = 0; lx < 8; ++lx) {
                     const int x = cxi * 8 + lx, y = cyi * 8 + ly;
@@ -137,7 +139,9 @@ int main(int argc, char** argv) {
                         }
                     }
                     float best = kMaxFloat;
+                    int scanned = 0;
                     for (auto& lf : leaves) {
+                        ++scanned;
                         const uint32_t c0 = C.range[2 * size_t(lf.second)], nc = C.range[2 * size_t(lf.second) + 1];
                         auto& u = used[lf.second];
                         u.resize(nc, 0);
@@ -158,7 +162,32 @@ int main(int argc, char** argv) {
                         }
                         if (improved) break;
                     }
+                    nleaves.push_back(scanned);
                 }
+            // wave step model: every live ray scans one leaf per step (now), or, once at most T rays
+            // are live, up to min(8, 64 / live) leaves each (tail speculation); a pass every 8 leaves
+            if (!nleaves.empty()) {
+                auto steps = [&](bool tail) {
+                    std::vector<int> left = nleaves, pos(nleaves.size(), 0);
+                    int st = 0;
+                    for (;;) {
+                        int live = 0;
+                        for (int x : left) live += x > 0;
+                        if (!live) break;
+                        ++st;
+                        const int S = tail && live <= 8 ? std::min(8, 64 / live) : 1;
+                        for (size_t i = 0; i < left.size(); ++i) {
+                            if (left[i] <= 0) continue;
+                            const int take = std::min(S, 8 - pos[i] % 8);  // not past the pass's buffer
+                            left[i] -= take;
+                            pos[i] += take;
+                        }
+                    }
+                    return st;
+                };
+                const int a = steps(false), b = steps(true);
+                cell_steps.push_back({a, b});
+            }
             for (auto& kv : used) {
                 const int nc = int(kv.second.size());
                 leaf_steps += 1;
@@ -174,6 +203,14 @@ int main(int argc, char** argv) {
                 union_clusters += uc;
             }
         }
+    std::sort(cell_steps.begin(), cell_steps.end());
+    const size_t nc = cell_steps.size();
+    double sa = 0, sb = 0;
+    for (auto& p : cell_steps) { sa += p.first; sb += p.second; }
+    std::printf("cells %zu: leaf steps per cell %.2f now, %.2f with tail speculation; slowest 1%%:", nc, sa / nc, sb / nc);
+    double ta = 0, tb = 0;
+    for (size_t k = nc - nc / 100; k < nc; ++k) { ta += cell_steps[k].first; tb += cell_steps[k].second; }
+    std::printf(" %.1f -> %.1f; max %d -> %d\n", ta / (nc / 100), tb / (nc / 100), cell_steps.back().first, cell_steps.back().second);
     std::printf("G=%d  leaf steps (cell, leaf) %.0f: cluster iterations now %.0f (%.2f per step), with superclusters %.0f (%.2f per step),"
                 " clusters some ray passes %.2f per step\n", G, leaf_steps, iters_now, iters_now / leaf_steps, iters_super,
                 iters_super / leaf_steps, union_clusters / leaf_steps);
