@@ -66,6 +66,18 @@ def assembly_index(plan: ShardPlan) -> np.ndarray:
     return dst
 
 
+def assembly_share(npixels: int, frame_ms: float, world: int, hbm_tbs: float = 5.0) -> float:
+    """Rank 0's frame assembly as a fraction of one rank's render of a frame (the plan's
+    rank0_extra): packing (4 B read, 3 written per pixel of its own shard) and the scatter of the
+    whole frame (3 B read, 8 B of index, 4 B written per pixel), HBM-bound at `hbm_tbs`, against
+    frame_ms / world of render (frame_ms: a calibration render of the whole frame). 0 without a
+    measurement. c3 at 8 ranks: ~0.1; c4: ~0.0003."""
+    if frame_ms <= 0.0 or world <= 1:
+        return 0.0
+    asm_ms = npixels * (7.0 / world + 15.0) / (hbm_tbs * 1e12) * 1e3
+    return min(0.5, asm_ms / (frame_ms / world))
+
+
 def tile_costs(eng, cam, width: int, height: int, side: int, seed: int) -> np.ndarray:
     """Measured cost (GPU shader clocks) of every grid tile: one calibration render."""
     return eng.tile_costs(cam, E.shard_grid(width, height, side), seed)

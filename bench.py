@@ -324,8 +324,9 @@ def main():
                     help="N>1 (and --single-tiles cost): each rank's tiles heaviest first (default) or in grid order")
     ap.add_argument("--single-tiles", default="frame", choices=["frame", "cost"],
                     help="N=1 tile list: one full-frame tile (default) or the shard grid, heaviest tiles first")
-    ap.add_argument("--rank0-extra", type=float, default=0.05,
-                    help="rank 0's frame-assembly share, as a fraction of the mean per-rank load")
+    ap.add_argument("--rank0-extra", type=float, default=-1.0,
+                    help="rank 0's frame-assembly share, as a fraction of the mean per-rank load; "
+                         "-1 (default): estimated from the calibration renders (S.assembly_share)")
     ap.add_argument("--exchange", default="bgr", choices=["bgr", "bgrx"],
                     help="N>1 frame exchange: 3 bytes per pixel (the framebuffer's X byte is always 0; "
                          "atr_pack_bgr / atr_scatter_bgr; gloo rehearsals stage the bytes through the host) or the "
@@ -372,7 +373,7 @@ def selftest(args):
     side = min(args.side, 32)
     n = len(S.E.shard_grid(W, H, side))
     costs = (np.arange(n) * 7919) % 97 + 1  # deterministic stand-in for the calibration render
-    plan = S.ShardPlan.balanced(costs, W, H, world, side, args.rank0_extra) if args.plan == "cost" \
+    plan = S.ShardPlan.balanced(costs, W, H, world, side, max(0.0, args.rank0_extra)) if args.plan == "cost" \
         else S.ShardPlan(W, H, world, side)
     F = args.frames_per_launch
     pix = torch.from_numpy(plan.pixel_map(rank).astype(np.int64)) if plan.sizes[rank] else torch.zeros(0, dtype=torch.int64)
@@ -508,9 +509,18 @@ def run(args):
         # just before them): a live renderer only has its previous frames
         ks = calib_frames(args)
         costs = np.zeros(len(E.shard_grid(W, H, args.side)), np.int64)
+        calib_ms = []
         if rank == 0:
             for k in ks:
+                torch.cuda.synchronize()
+                t_ = time.perf_counter()
                 costs += S.tile_costs(eng, cams[k % n_orbit], W, H, args.side, SEED)
+                calib_ms.append((time.perf_counter() - t_) * 1e3)
+        if args.rank0_extra < 0:  # rank 0's assembly against a rank's render, from the calibration
+            args.rank0_extra = S.assembly_share(W * H, float(np.median(calib_ms)) if calib_ms else 0.0, pw)
+            if world > 1:
+                args.rank0_extra = float(S.shared_costs(np.array([int(args.rank0_extra * 1e6)]), rank, dist,
+                                                        dev if backend == "nccl" else "cpu")[0]) / 1e6
         if world > 1:
             costs = S.shared_costs(costs, rank, dist, dev if backend == "nccl" else "cpu")
         plan = S.ShardPlan.balanced(costs, W, H, pw, args.side, args.rank0_extra, heavy_first)
@@ -851,6 +861,7 @@ def run(args):
                           "streams": args.streams, "frames_per_launch": F_,
                           **({"exchange": "bgr (3 B/px)" if bgr else "bgrx (4 B/px)"} if pw > 1 else {}),
                           "launches": launch_sizes(args.steps, F_, S_),
+                          **({"rank0_extra": round(args.rank0_extra, 4)} if pw > 1 else {}),
                           "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),
                           "cell_plan": cell_split,
                           "shard_pixels": [int(x) for x in sizes]},

@@ -171,3 +171,15 @@ def test_bgr_pack_scatter_host_roundtrip():
     assert np.array_equal(img[perm], fb)
     with pytest.raises(AssertionError):
         pack_bgr_host(np.array([1 << 24], np.uint32))
+
+
+def test_assembly_share():
+    """rank 0's assembly against a rank's render (bench.py's default rank0_extra): HBM-bound pack +
+    scatter of the frame vs frame_ms / world; 0 without a measurement or at one rank."""
+    from atray_amd.shard import assembly_share
+    n = 1920 * 1080
+    c3 = assembly_share(n, 0.34, 8)        # a 0.34-ms calibration frame over 8 ranks
+    c4 = assembly_share(n, 69.0, 8)
+    assert 0.1 < c3 < 0.2 and 0.0 < c4 < 0.001
+    assert assembly_share(n, 0.0, 8) == 0.0 and assembly_share(n, 0.34, 1) == 0.0
+    assert assembly_share(n, 1e-6, 8) == 0.5  # capped
