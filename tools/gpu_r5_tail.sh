@@ -15,5 +15,7 @@ for i in 1 2; do
   run one_stream_$i --streams 1
   run four_launch_$i --frames-per-launch 5
   run one_launch10_$i --streams 1 --frames-per-launch 10 --steps 10
+  run list_grid_$i --cell-order list --tile-order grid
+  run list_cost_$i --cell-order list
 done
 echo all done
