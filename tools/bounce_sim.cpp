@@ -97,6 +97,10 @@ struct Walk { double rays = 0, ref_visits = 0, lazy_visits = 0, lazy_pq_visits =
 Walk g_walk[3];
 int g_level = 0;
 int g_min_safe = 1;  // lazy_restart: safe leaves a pass returns at least (argv[4])
+// per traced ray of the current level, for the wave model: the kernel's passes (visits, leaves
+// consumed) and the lazy walk's visits before each leaf it scans
+struct RaySeq { std::vector<std::pair<int, int>> k8; std::vector<int> lazy; };
+std::vector<RaySeq> g_seq[3];
 
 // Inner-node visits of three traversal schedules for the same query (the leaf set and order are the
 // reference's; only the visiting differs):
@@ -291,6 +295,8 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
         std::vector<Pend> pend{{0.f, S.rlo[0], 0}};
         std::vector<std::pair<float, int32_t>> found;  // sorted (dist, rank)
         double visits = 0;
+        int since = 0;  // visits since the last leaf scan
+        std::vector<int> seq;
         bool done = false;
         while (!done) {
             // scan every safe leaf
@@ -299,6 +305,8 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
                 for (const Pend& p : pend)
                     if (!lex_less(found[0].first, found[0].second, p.bound, p.rlo)) { safe = false; break; }
                 if (!safe) break;
+                seq.push_back(since);
+                since = 0;
                 if (found[0].second == stop_rank) { done = true; break; }
                 found.erase(found.begin());
             }
@@ -310,6 +318,7 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
             const Pend p = pend[pick];
             pend.erase(pend.begin() + long(pick));
             visits += 1;
+            ++since;
             Examined e = examine(S, o, inv, p.node);
             for (auto& lf : e.leaves) {
                 auto it = std::lower_bound(found.begin(), found.end(), lf, [](const std::pair<float, int32_t>& a,
@@ -322,6 +331,16 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
             for (auto it = e.inner.rbegin(); it != e.inner.rend(); ++it) pend.push_back(*it);
         }
         (pq ? W.lazy_pq_visits : W.lazy_visits) += visits;
+        if (!pq) {
+            while (!found.empty() && !done) {  // no pending subtree left: the rest are safe
+                seq.push_back(since);
+                since = 0;
+                if (found[0].second == stop_rank) break;
+                found.erase(found.begin());
+            }
+            g_seq[g_level].emplace_back();
+            g_seq[g_level].back().lazy = seq;
+        }
     }
     // lazy_restart: near-first passes that return as soon as some found leaf is safe (every safe leaf,
     // at most K), the leaves scanned, then a re-walk from the root after the last returned leaf
@@ -377,8 +396,10 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
         float bd = -1e30f;
         int32_t bi = -1;
         double visits = 0;
+        std::vector<std::pair<int, int>> passes;
         for (;;) {
             W.k8_passes += 1;
+            const double v0 = visits;
             std::vector<std::pair<float, int32_t>> buf;  // sorted, at most K
             bool more = false;
             std::vector<Pend> st{{0.f, S.rlo[0], 0}};
@@ -403,13 +424,18 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
                 for (auto it = e.inner.rbegin(); it != e.inner.rend(); ++it) st.push_back(*it);
             }
             bool stop = false;
-            for (auto& lf : buf)
+            int used = 0;
+            for (auto& lf : buf) {
+                ++used;
                 if (lf.second == stop_rank) { stop = true; break; }
+            }
+            passes.push_back({int(visits - v0), used});
             if (stop || !more || buf.empty()) break;
             bd = buf.back().first;
             bi = buf.back().second;
         }
         W.k8_visits += visits;
+        g_seq[g_level].back().k8 = passes;
     }
     (void)ref_leaves;
 }
@@ -502,6 +528,53 @@ int main(int argc, char** argv) {
                     c.far / a, c.uv / a, c.culled / a, c.origin_leaf_full / a, c.plane_keep / a, c.sphere_keep / a,
                     c.both_keep / a);
     };
+    // wave model: rays in generation order, 64 per wave (level 1: a pixel's samples side by side)
+    for (int l = 1; l < 3; ++l) {
+        const auto& R = g_seq[l];
+        double k8_iters = 0, k8_steps = 0, lz_iters = 0, lz_steps = 0, waves = 0;
+        for (size_t w0 = 0; w0 + 64 <= R.size(); w0 += 64) {
+            waves += 1;
+            {   // the kernel: a pass phase whenever a lane needs a pass (all lanes wait), then a leaf step
+                std::vector<size_t> p(64, 0);
+                std::vector<int> c(64, 0);
+                std::vector<char> need(64, 1), done(64, 0);
+                for (int i = 0; i < 64; ++i) if (R[w0 + i].k8.empty()) done[i] = 1, need[i] = 0;
+                for (;;) {
+                    int mx = 0, live = 0;
+                    for (int i = 0; i < 64; ++i)
+                        if (!done[i] && need[i]) { mx = std::max(mx, R[w0 + i].k8[p[i]].first); need[i] = 0; }
+                    for (int i = 0; i < 64; ++i) live += !done[i];
+                    if (!live) break;
+                    k8_iters += mx;
+                    k8_steps += 1;
+                    for (int i = 0; i < 64; ++i) {
+                        if (done[i]) continue;
+                        const auto& ps = R[w0 + i].k8;
+                        if (++c[i] >= ps[p[i]].second) {
+                            if (p[i] + 1 < ps.size()) { ++p[i]; c[i] = 0; need[i] = 1; }
+                            else done[i] = 1;
+                        }
+                    }
+                }
+            }
+            {   // lazy: before each leaf step, every live lane walks until its next leaf is safe
+                std::vector<size_t> q(64, 0);
+                for (;;) {
+                    int mx = 0, live = 0;
+                    for (int i = 0; i < 64; ++i) {
+                        const auto& z = R[w0 + i].lazy;
+                        if (q[i] < z.size()) { ++live; mx = std::max(mx, z[q[i]]); }
+                    }
+                    if (!live) break;
+                    lz_iters += mx;
+                    lz_steps += 1;
+                    for (int i = 0; i < 64; ++i) if (q[i] < R[w0 + i].lazy.size()) ++q[i];
+                }
+            }
+        }
+        std::printf("level %d wave model (%.0f waves): DFS wave iterations %.1f -> %.1f lazy; leaf steps %.1f -> %.1f\n",
+                    l, waves, k8_iters / waves, lz_iters / waves, k8_steps / waves, lz_steps / waves);
+    }
     for (int l = 0; l < 3; ++l) {
         const Walk& w = g_walk[l];
         std::printf("level %d inner-node visits per ray: reference %.2f  k8 passes %.2f (%.2f passes)  lazy %.2f  lazy (priority) %.2f"
