@@ -99,7 +99,7 @@ int g_level = 0;
 int g_min_safe = 1;  // lazy_restart: safe leaves a pass returns at least (argv[4])
 // per traced ray of the current level, for the wave model: the kernel's passes (visits, leaves
 // consumed) and the lazy walk's visits before each leaf it scans
-struct RaySeq { std::vector<std::pair<int, int>> k8; std::vector<int> lazy; };
+struct RaySeq { std::vector<std::pair<int, int>> k8; std::vector<int> lazy; float o[3], d[3]; int oleaf = -1; };
 std::vector<RaySeq> g_seq[3];
 
 // Inner-node visits of three traversal schedules for the same query (the leaf set and order are the
@@ -339,7 +339,16 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
                 found.erase(found.begin());
             }
             g_seq[g_level].emplace_back();
-            g_seq[g_level].back().lazy = seq;
+            RaySeq& rs = g_seq[g_level].back();
+            rs.lazy = seq;
+            rs.o[0] = o.x; rs.o[1] = o.y; rs.o[2] = o.z;
+            rs.d[0] = d.x; rs.d[1] = d.y; rs.d[2] = d.z;
+            // the leaf holding the origin (the first leaf of the reference order whose box contains o)
+            for (int32_t n = 0; n < T.nnodes && rs.oleaf < 0; ++n) {
+                if (T.children[size_t(n)]) continue;
+                const float* b = &T.bounds[6 * size_t(n)];
+                if (o.x >= b[0] && o.x <= b[3] && o.y >= b[1] && o.y <= b[4] && o.z >= b[2] && o.z <= b[5]) rs.oleaf = n;
+            }
         }
     }
     // lazy_restart: near-first passes that return as soon as some found leaf is safe (every safe leaf,
@@ -529,8 +538,23 @@ int main(int argc, char** argv) {
                     c.both_keep / a);
     };
     // wave model: rays in generation order, 64 per wave (level 1: a pixel's samples side by side)
-    for (int l = 1; l < 3; ++l) {
-        const auto& R = g_seq[l];
+    for (int l = 1; l < 3; ++l)
+      for (int order = 0; order < 4; ++order) {
+        // 0: queue order; 1: sorted by (origin leaf, direction octant); 2: by direction octant then
+        // origin leaf; 3: by a 64-bin direction cell (octant x 8 sub-cells) then origin leaf
+        std::vector<RaySeq> R = g_seq[l];
+        auto oct = [](const RaySeq& r) { return (r.d[0] < 0) * 4 + (r.d[1] < 0) * 2 + (r.d[2] < 0); };
+        auto cell = [&](const RaySeq& r) {
+            const float ax = std::fabs(r.d[0]), ay = std::fabs(r.d[1]), az = std::fabs(r.d[2]);
+            const int major = ax >= ay && ax >= az ? 0 : (ay >= az ? 1 : 2);
+            return oct(r) * 8 + major * 2 + (std::max(ax, std::max(ay, az)) > 0.85f);
+        };
+        if (order == 1) std::stable_sort(R.begin(), R.end(), [&](const RaySeq& a, const RaySeq& b) {
+            return a.oleaf != b.oleaf ? a.oleaf < b.oleaf : oct(a) < oct(b); });
+        if (order == 2) std::stable_sort(R.begin(), R.end(), [&](const RaySeq& a, const RaySeq& b) {
+            return oct(a) != oct(b) ? oct(a) < oct(b) : a.oleaf < b.oleaf; });
+        if (order == 3) std::stable_sort(R.begin(), R.end(), [&](const RaySeq& a, const RaySeq& b) {
+            return cell(a) != cell(b) ? cell(a) < cell(b) : a.oleaf < b.oleaf; });
         double k8_iters = 0, k8_steps = 0, lz_iters = 0, lz_steps = 0, waves = 0;
         for (size_t w0 = 0; w0 + 64 <= R.size(); w0 += 64) {
             waves += 1;
@@ -572,8 +596,8 @@ int main(int argc, char** argv) {
                 }
             }
         }
-        std::printf("level %d wave model (%.0f waves): DFS wave iterations %.1f -> %.1f lazy; leaf steps %.1f -> %.1f\n",
-                    l, waves, k8_iters / waves, lz_iters / waves, k8_steps / waves, lz_steps / waves);
+        std::printf("level %d order %d wave model (%.0f waves): DFS wave iterations %.1f -> %.1f lazy; leaf steps %.1f -> %.1f\n",
+                    l, order, waves, k8_iters / waves, lz_iters / waves, k8_steps / waves, lz_steps / waves);
     }
     for (int l = 0; l < 3; ++l) {
         const Walk& w = g_walk[l];
