@@ -33,6 +33,7 @@ extern "C" hipError_t atr_launch_unpack(const atr::DBlock* blocks, int32_t nbloc
 extern "C" hipError_t atr_launch_path_camera(const atr::PathParams& P, int occ, hipStream_t s);
 extern "C" hipError_t atr_launch_path_bounce(const atr::PathParams& P, int ncu, int occ, hipStream_t s);
 extern "C" hipError_t atr_launch_path_resolve(const atr::PathParams& P, hipStream_t s);
+extern "C" hipError_t atr_launch_path_sort(const atr::PathParams& P, int ncu, hipStream_t s);
 extern "C" hipError_t atr_launch_tile_casts(const atr_tile* tiles, int32_t ntiles, int32_t width,
                                             const uint32_t* casts, int64_t* out, hipStream_t s);
 extern "C" hipError_t atr_launch_packed_tile_casts(const int32_t* slot_tile, int64_t nslots, const uint32_t* casts,
@@ -212,6 +213,7 @@ struct atr_ctx {
     DScene* d_scene = nullptr;
     int64_t scene_bytes = 0;
     int32_t max_nodes = 0, max_depth = 0, nmodels = 0, max_inner = 0;
+    float scene_box[6] = {0.f, 0.f, 0.f, 1.f, 1.f, 1.f};  // the models' vertex bounds (lo, hi): queue-sort cells
     atr_tuning tune = default_tuning();  // atr_set_tuning
     int64_t nclusters = 0;
     // per-cell plan (atr_set_cell_plan) for images of cplan_w x cplan_h; cplan_gen invalidates
@@ -232,6 +234,7 @@ struct atr_ctx {
         DevBuf mem;
         int64_t cap = 0;
         int32_t levels = 0;
+        bool sort = false;        // holds the queue-sort buffers (PathSort)
         hipEvent_t ev = nullptr;  // recorded after the latest launch that used `mem`
         uint64_t last_use = 0;
     };
@@ -481,7 +484,17 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
 // its own last launch only. When the device has no memory for it, idle workspaces of other streams
 // are released and the allocation retried once; hipErrorOutOfMemory then goes back to the caller
 // (launch_paths halves its batch, launch_kernels falls back to FLAT).
-hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, atr_ctx::PathWS*& out) {
+// Queue-sort buffers after the queues and counters: {key, rank} and the key order per entry, the
+// bins, their starts and block sums (for kMaxSortBits), 256-B aligned.
+size_t sort_offset(int64_t cap, int32_t levels) {
+    return (size_t(cap) * 16 * (2 * kPathPlanes + 1) + size_t(levels) * sizeof(PathCtl) + 255) & ~size_t(255);
+}
+constexpr int64_t kSortBinsMax = int64_t(64) << (3 * kMaxSortBits);
+size_t sort_bytes(int64_t cap) {
+    return size_t(cap) * 12 + size_t(kSortBinsMax) * 8 + size_t(kSortBinsMax / kSortChunk) * 4;
+}
+
+hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, bool sort, atr_ctx::PathWS*& out) {
     atr_ctx::PathWS* ws = nullptr;
     hipError_t e;
     for (auto& w : c->path_ws)
@@ -502,16 +515,20 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
     if (ws->stream != s && ws->mem.p && (e = hipStreamWaitEvent(s, ws->ev, 0)) != hipSuccess) return e;
     ws->stream = s;
     ws->last_use = ++c->ws_clock;
-    if (ws->cap < cap || ws->levels < levels) {
+    if (ws->cap < cap || ws->levels < levels || (sort && !ws->sort)) {
         if ((e = hipEventSynchronize(ws->ev)) != hipSuccess) return e;
         if (ws->mem.p && (e = hipFree(ws->mem.p)) != hipSuccess) return e;
         ws->mem = DevBuf();
         const int64_t ncap = std::max(ws->cap, cap);
         const int32_t nlev = std::max(ws->levels, levels);
+        const bool nsort = ws->sort || sort;
         ws->cap = 0;
         ws->levels = 0;
-        // 2 queues x kPathPlanes planes + the per-path results, 16 B per entry; the level counters
-        const size_t bytes = size_t(ncap) * 16 * (2 * kPathPlanes + 1) + size_t(nlev) * sizeof(PathCtl);
+        ws->sort = false;
+        // 2 queues x kPathPlanes planes + the per-path results, 16 B per entry; the level counters;
+        // the queue-sort buffers
+        const size_t bytes = nsort ? sort_offset(ncap, nlev) + sort_bytes(ncap)
+                                   : size_t(ncap) * 16 * (2 * kPathPlanes + 1) + size_t(nlev) * sizeof(PathCtl);
         e = hipMalloc(&ws->mem.p, bytes);
         if (e == hipErrorOutOfMemory) {
             (void)hipGetLastError();
@@ -521,6 +538,7 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
                     w.mem = DevBuf();
                     w.cap = 0;
                     w.levels = 0;
+                    w.sort = false;
                 }
             e = hipMalloc(&ws->mem.p, bytes);
         }
@@ -532,6 +550,7 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
         ws->mem.n = bytes;
         ws->cap = ncap;
         ws->levels = nlev;
+        ws->sort = nsort;
     }
     out = ws;
     return hipSuccess;
@@ -547,6 +566,8 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     if (bl > kMaxPathBounces) return hipErrorInvalidValue;
     const int64_t per_cell = 64 * std::max<int64_t>(spp, 1);
     const int32_t levels = std::max(bl, 1);
+    // the queue sort pays off only when a level's queue feeds another bounce launch
+    const int32_t sort_bits = bl >= 2 ? c->tune.path_sort_bits : 0;
     atr_ctx::PathWS* ws = nullptr;
     hipError_t e = hipErrorOutOfMemory;
     int64_t cells = 0;
@@ -560,7 +581,7 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
         int64_t cap = 1;
         while (cap < cells * per_cell) cap <<= 1;
         cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
-        e = path_workspace(c, s, cap, std::max(levels, 8), ws);
+        e = path_workspace(c, s, cap, std::max(levels, 8), sort_bits > 0, ws);
         if (e == hipSuccess && ws->cap < cap) e = hipErrorOutOfMemory;
     }
     if (e != hipSuccess) return e;
@@ -594,14 +615,40 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     Q.hyb_b = P.hyb_b;
     Q.nfcam = P.nfcam;
     for (int32_t f = 0; f < P.nfcam; ++f) Q.fcam[f] = P.fcam[f];
+    if (sort_bits > 0) {
+        PathSort& so = Q.sort;
+        so.bits = sort_bits;
+        so.nbins = int32_t(64) << (3 * sort_bits);
+        const float* box = c->scene_box;
+        for (int a = 0; a < 3; ++a) {
+            so.lo[a] = box[a];
+            const float ext = box[3 + a] - box[a];
+            so.sc[a] = ext > 0.0f ? float(1 << sort_bits) / ext : 0.0f;
+        }
+        char* sb = static_cast<char*>(ws->mem.p) + sort_offset(ws->cap, ws->levels);
+        so.kr = reinterpret_cast<uint2_t*>(sb);
+        sb += size_t(ws->cap) * 8;
+        so.perm = reinterpret_cast<uint32_t*>(sb);
+        sb += size_t(ws->cap) * 4;
+        so.hist = reinterpret_cast<uint32_t*>(sb);
+        so.start = so.hist + kSortBinsMax;
+        so.part = so.start + kSortBinsMax;
+    }
     const int occ_cam = c->tune.path_camera_occ, occ_bounce = c->tune.path_bounce_occ;
     for (int64_t c0 = 0; c0 < P.nblocks; c0 += cells) {
         Q.cell0 = int32_t(c0);
         Q.ncells = int32_t(std::min<int64_t>(cells, P.nblocks - c0));
         if (bl > 0 && spp > 0) {
             if ((e = hipMemsetAsync(Q.ctl, 0, sizeof(PathCtl) * size_t(levels), s)) != hipSuccess) return e;
+            if (sort_bits > 0 &&
+                (e = hipMemsetAsync(Q.sort.hist, 0, sizeof(uint32_t) * size_t(Q.sort.nbins), s)) != hipSuccess)
+                return e;
             if ((e = atr_launch_path_camera(Q, occ_cam, s)) != hipSuccess) return e;
             for (int32_t k = 1; k < bl; ++k) {
+                if (sort_bits > 0) {  // level k - 1's queue in key order (the launches zero the bins)
+                    Q.bounce = k - 1;
+                    if ((e = atr_launch_path_sort(Q, c->ncu, s)) != hipSuccess) return e;
+                }
                 Q.bounce = k;
                 if ((e = atr_launch_path_bounce(Q, c->ncu, occ_bounce, s)) != hipSuccess) return e;
             }
@@ -922,7 +969,8 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
         t->path_batch_log2 < 12 || t->path_batch_log2 > 28 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
         t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
         (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)) ||
-        (t->primary_occ != 0 && (t->primary_occ < 6 || t->primary_occ > 8)))
+        (t->primary_occ != 0 && (t->primary_occ < 6 || t->primary_occ > 8)) ||
+        (t->path_sort_bits != 0 && (t->path_sort_bits < 2 || t->path_sort_bits > kMaxSortBits)))
         return ATR_E_INVALID;
     for (int32_t r : t->reserved)
         if (r) return ATR_E_INVALID;
@@ -1004,6 +1052,14 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
     c->max_depth = 0;
     c->max_inner = 0;
     c->nclusters = 0;
+    float box[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int32_t i = 0; i < nmodels; ++i)
+        for (const V3& v : models[i].mesh->m.vertices) {
+            box[0] = std::min(box[0], v.x), box[1] = std::min(box[1], v.y), box[2] = std::min(box[2], v.z);
+            box[3] = std::max(box[3], v.x), box[4] = std::max(box[4], v.y), box[5] = std::max(box[5], v.z);
+        }
+    if (box[0] <= box[3] && box[1] <= box[4] && box[2] <= box[5])
+        std::memcpy(c->scene_box, box, sizeof(box));
     for (int32_t i = 0; i < nmodels; ++i) {
         const atr_model& md = models[i];
         const HostMesh& M = md.mesh->m;
@@ -1562,7 +1618,8 @@ int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
     HIPCHK(hipMemcpy(&err, c->d_error, sizeof(err), hipMemcpyDeviceToHost));
     if (err) {
         HIPCHK(hipMemset(c->d_error, 0, sizeof(int32_t)));
-        return ATR_E_TREE_DEPTH;
+        // bit 1: a queue-sort slot outside its level (paths.hip path_sort_rank; never expected)
+        return (err & 2) ? -(1000 + int(hipErrorUnknown)) : ATR_E_TREE_DEPTH;
     }
     if (tiles_done) *tiles_done = c->last_ntiles;
     return ATR_OK;

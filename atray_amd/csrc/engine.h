@@ -216,6 +216,28 @@ struct PathCtl {
     uint32_t tail;
     uint32_t head;
 };
+// Queue sort (tuning path_sort_bits = b > 0): the queues are entry-major (an entry's
+// four records together, q[4 e + i], 64 B) and every queued path also records {key, rank} in `kr`:
+// key = the ray's direction cell (octant x dominant axis x steep, 6 bits) above a Morton code of its
+// origin quantised to b bits per axis over the scene box (lo, sc = 2^b / extent), rank = its arrival
+// in the key's bin (atomicAdd on hist). The sort launches turn hist into bin starts and write the
+// level's key order perm[start[key] + rank] = entry; the next bounce launch's waves claim positions
+// of that order, so a wavefront takes rays of one direction cell and one region together (a
+// counting sort of 4-B indices; the entries never move; the order within a bin is arrival order,
+// and no output depends on queue order).
+constexpr int kMaxSortBits = 7;
+constexpr int32_t kSortChunk = 4096;  // bins per block of the bin scan
+struct PathSort {
+    int32_t bits;      // 0: off
+    int32_t nbins;     // 64 << 3 bits
+    float lo[3], sc[3];
+    uint2_t* kr;       // {key, rank} per entry of the level being written
+    uint32_t* perm;    // the previous level's key order (entry per position)
+    uint32_t* hist;    // nbins arrival counters (zero between levels)
+    uint32_t* start;   // nbins bin starts
+    uint32_t* part;    // nbins / kSortChunk block sums
+};
+
 struct PathParams {
     atr_camera cam;
     const DScene* scene;
@@ -243,6 +265,7 @@ struct PathParams {
     int32_t xcd_chunk;
     int32_t hyb_a, hyb_b;
     int32_t nfcam;
+    PathSort sort;
     atr_camera fcam[kMaxFrameCams];
 };
 

@@ -22,6 +22,10 @@
 
 #include "scan.h"
 
+#ifndef ATR_SORT_KEY
+#define ATR_SORT_KEY 0
+#endif
+
 namespace atr {
 
 // (The helpers take plain values: a reference to the kernel argument passed to a function made the
@@ -48,10 +52,54 @@ __device__ __forceinline__ void path_finish(float4_t* out, uint32_t o, V3 ret, u
     out[o] = float4_t{ret.x, ret.y, ret.z, __uint_as_float(casts)};
 }
 
+// Sort key of a queued ray (PathSort, engine.h): direction cell (octant, dominant axis, |d| of that
+// axis above 0.85) above the Morton code of its origin's cell, b bits per axis over the scene box.
+__device__ __forceinline__ uint32_t spread3(uint32_t x) {  // bits 0..9 -> every third bit
+    x = (x | (x << 16)) & 0x030000FFu;
+    x = (x | (x << 8)) & 0x0300F00Fu;
+    x = (x | (x << 4)) & 0x030C30C3u;
+    return (x | (x << 2)) & 0x09249249u;
+}
+__device__ __forceinline__ uint32_t path_sort_morton(V3 o, PathSort so) {
+    const float qmax = float((1 << so.bits) - 1);
+    // fmaxf first: a NaN coordinate lands in cell 0
+    const uint32_t qx = uint32_t(fminf(fmaxf((o.x - so.lo[0]) * so.sc[0], 0.0f), qmax));
+    const uint32_t qy = uint32_t(fminf(fmaxf((o.y - so.lo[1]) * so.sc[1], 0.0f), qmax));
+    const uint32_t qz = uint32_t(fminf(fmaxf((o.z - so.lo[2]) * so.sc[2], 0.0f), qmax));
+    return (spread3(qx) << 2) | (spread3(qy) << 1) | spread3(qz);
+}
+__device__ __forceinline__ uint32_t path_sort_key(V3 o, V3 d, PathSort so) {
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const uint32_t oct = (d.x < 0.0f ? 4u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 1u : 0u);
+    const uint32_t major = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
+    const uint32_t steep = fmaxf(ax, fmaxf(ay, az)) > 0.85f ? 1u : 0u;
+#if ATR_SORT_KEY == 2  // experiment: an octahedral 8 x 8 direction cell
+    {
+        const float sum = ax + ay + az;
+        float u = d.x / sum, v = d.y / sum;
+        if (d.z < 0.0f) {
+            const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+            v = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+            u = uu;
+        }
+        const uint32_t iu = uint32_t(fminf(fmaxf((u * 0.5f + 0.5f) * 8.0f, 0.0f), 7.0f));
+        const uint32_t iv = uint32_t(fminf(fmaxf((v * 0.5f + 0.5f) * 8.0f, 0.0f), 7.0f));
+        (void)oct, (void)major, (void)steep;
+        return ((iv * 8u + iu) << (3 * so.bits)) | path_sort_morton(o, so);
+    }
+#elif ATR_SORT_KEY == 1  // experiment: origin cell above the direction cell
+    return (path_sort_morton(o, so) << 6) | (oct << 3) | (major << 1) | steep;
+#else
+    return (((oct << 3) | (major << 1) | steep) << (3 * so.bits)) | path_sort_morton(o, so);
+#endif
+}
+
 // Append this lane's path (if `go`) to queue q (planes `cap` entries apart): one atomic per wave for
-// the wave's survivors, each at base + its rank among them.
+// the wave's survivors, each at base + its rank among them. With the queue sort on, the entry also
+// records its key and its rank in the key's bin (PathSort).
+template <bool SORT>
 __device__ __forceinline__ void path_enqueue(float4_t* q, int64_t cap, PathCtl* ctl, bool go, V3 o, V3 d,
-                                             uint32_t pix, uint32_t g, V3 ret, V3 w, uint64_t st) {
+                                             uint32_t pix, uint32_t g, V3 ret, V3 w, uint64_t st, PathSort so) {
     const uint64_t m = __ballot(go);
     if (m == 0) return;
     const int lane = threadIdx.x & 63;
@@ -60,10 +108,17 @@ __device__ __forceinline__ void path_enqueue(float4_t* q, int64_t cap, PathCtl* 
     base = uint32_t(__builtin_amdgcn_readfirstlane(int(__shfl(int(base), 0))));
     if (!go) return;
     const int64_t e = int64_t(base) + __popcll(m & ((uint64_t(1) << lane) - 1));
-    q[e] = float4_t{o.x, o.y, o.z, d.x};
-    q[cap + e] = float4_t{d.y, d.z, __uint_as_float(pix), __uint_as_float(g)};
-    q[2 * cap + e] = float4_t{ret.x, ret.y, ret.z, w.x};
-    q[3 * cap + e] = float4_t{w.y, w.z, __uint_as_float(uint32_t(st)), __uint_as_float(uint32_t(st >> 32))};
+    // sorted queues hold each entry's four records together (64 B, entry-major: q[4 e + i]) so the
+    // sort moves whole 64-B blocks; unsorted queues keep the four planes (q[i cap + e])
+    const int64_t e0 = SORT ? 4 * e : e, es = SORT ? 1 : cap;
+    if constexpr (SORT) {
+        const uint32_t key = path_sort_key(o, d, so);
+        so.kr[e] = uint2_t{key, atomicAdd(so.hist + key, 1u)};
+    }
+    q[e0] = float4_t{o.x, o.y, o.z, d.x};
+    q[es + e0] = float4_t{d.y, d.z, __uint_as_float(pix), __uint_as_float(g)};
+    q[2 * es + e0] = float4_t{ret.x, ret.y, ret.z, w.x};
+    q[3 * es + e0] = float4_t{w.y, w.z, __uint_as_float(uint32_t(st)), __uint_as_float(uint32_t(st >> 32))};
 }
 
 template <bool COUNT>
@@ -97,7 +152,7 @@ __device__ __forceinline__ void path_counters(unsigned long long* C, const Ctr& 
 }
 
 // ------------------------------------------------------------------ camera rays + first shading
-template <bool COUNT, int OCC>
+template <bool COUNT, int OCC, bool SORT>
 __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const uint32_t spp = uint32_t(__builtin_amdgcn_readfirstlane(int(P.cam.samples_per_pixel)));
@@ -156,7 +211,7 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
             else go = true;
         }
     }
-    path_enqueue(P.q[0], P.cap, &P.ctl[0], go, o, d, uint32_t(pix), g, ret, w, st);
+    path_enqueue<SORT>(P.q[0], P.cap, &P.ctl[0], go, o, d, uint32_t(pix), g, ret, w, st, P.sort);
     const uint32_t traced = active ? 1u : 0u;
     if (P.traced_rays) add_traced(P.traced_rays, traced, int(wv));
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
@@ -169,7 +224,7 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
 // LDS to 18 KB per workgroup, enough for 8 waves/SIMD, but cost re-walks: c4 71.0 ms per frame at 7
 // waves and 72.1 at 8 (64 VGPRs, scratch in the hot loop) vs 69.5 with 8 entries.
 constexpr int kBounceLeafBuf = kLeafBuf;
-template <bool COUNT, int OCC>
+template <bool COUNT, int OCC, bool SORT>
 __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
     const int lane = threadIdx.x & 63;
     const int32_t k = P.bounce;  // 1 .. bounce_limit - 1
@@ -187,11 +242,14 @@ __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
         base = uint32_t(__builtin_amdgcn_readfirstlane(int(__shfl(int(base), 0))));
         if (base >= n) break;
         const uint64_t clk0 = P.block_cost ? clock64() : 0;
-        const uint32_t e = base + uint32_t(lane);
-        const bool valid = e < n;
+        const uint32_t i = base + uint32_t(lane);
+        const bool valid = i < n;
+        // sorted queues: claimed position i of the level's key order -> its entry (PathSort)
+        uint32_t e = i;
+        if (SORT && valid) e = P.sort.perm[i];
         V3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
         if (valid) {
-            const float4_t a = qin[e], b = qin[P.cap + e];
+            const float4_t a = qin[SORT ? 4 * int64_t(e) : e], b = qin[SORT ? 4 * int64_t(e) + 1 : P.cap + e];
             o = mk(a.x, a.y, a.z);
             d = mk(a.w, b.x, b.y);
         }
@@ -207,7 +265,8 @@ __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
         uint64_t st = 0;
         if (valid) {
             traced += 1;
-            const float4_t a = qin[ea], b = qin[P.cap + ea], c = qin[2 * P.cap + ea], q3 = qin[3 * P.cap + ea];
+            const int64_t e0 = SORT ? 4 * int64_t(ea) : ea, es = SORT ? 1 : P.cap;
+            const float4_t a = qin[e0], b = qin[es + e0], c = qin[2 * es + e0], q3 = qin[3 * es + e0];
             o = mk(a.x, a.y, a.z);
             d = mk(a.w, b.x, b.y);
             Isect id;
@@ -235,7 +294,7 @@ __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
                 atomicAdd(P.block_cost + P.blocks[bi].base, (unsigned long long)((clock64() - clk0) / nv));
             }
         }
-        path_enqueue(P.q[k & 1], P.cap, &P.ctl[k], go, o, d, pix, g, ret, w, st);
+        path_enqueue<SORT>(P.q[k & 1], P.cap, &P.ctl[k], go, o, d, pix, g, ret, w, st, P.sort);
     }
     if (P.traced_rays) add_traced(P.traced_rays, traced, int(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (err && P.error_flag) atomicOr(P.error_flag, 1);
@@ -283,46 +342,164 @@ __global__ __launch_bounds__(256) void path_resolve_kernel(PathParams P) {
     if (P.ray_casts) P.ray_casts[o] = casts;
 }
 
+// ------------------------------------------------------------------ queue sort (PathSort)
+// Level k's bins: block b sums hist[b x kSortChunk ..) into part[b].
+__global__ __launch_bounds__(256) void path_sort_sums(PathSort so) {
+    const uint4_t* h = reinterpret_cast<const uint4_t*>(so.hist + int64_t(blockIdx.x) * kSortChunk);
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < kSortChunk / 1024; ++i) {
+        const uint4_t v = h[i * 256 + threadIdx.x];
+        t += v.x + v.y + v.z + v.w;
+    }
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    __shared__ uint32_t ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) so.part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// The block sums' exclusive scan, in place (one workgroup; nbins / kSortChunk <= 2^15 sums).
+__global__ __launch_bounds__(1024) void path_sort_part_scan(PathSort so) {
+    __shared__ uint32_t ws[16];
+    const int n = so.nbins / kSortChunk, per = (n + 1023) / 1024;
+    const int i0 = int(threadIdx.x) * per, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t t = 0;
+    for (int i = i0; i < i0 + per && i < n; ++i) t += so.part[i];
+    uint32_t inc = t;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - t;
+    for (int w = 0; w < wave; ++w) run += ws[w];
+    for (int i = i0; i < i0 + per && i < n; ++i) {
+        const uint32_t v = so.part[i];
+        so.part[i] = run;
+        run += v;
+    }
+}
+
+// Block b: its bins' exclusive starts (its block's start, then a scan of its own kSortChunk bins,
+// 16 per thread), and the bins zeroed for the next level.
+__global__ __launch_bounds__(256) void path_sort_scan(PathSort so) {
+    __shared__ uint32_t ws[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t pre = so.part[blockIdx.x];
+    uint4_t* h = reinterpret_cast<uint4_t*>(so.hist + int64_t(blockIdx.x) * kSortChunk) + 4 * threadIdx.x;
+    uint4_t* st = reinterpret_cast<uint4_t*>(so.start + int64_t(blockIdx.x) * kSortChunk) + 4 * threadIdx.x;
+    uint4_t v[4];
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[i] = h[i];
+        t += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+    uint32_t inc = t;  // inclusive scan over the wave, then over the four waves
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t run = pre + inc - t;
+    for (int w = 0; w < wave; ++w) run += ws[w];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint4_t o;
+        o.x = run; run += v[i].x;
+        o.y = run; run += v[i].y;
+        o.z = run; run += v[i].z;
+        o.w = run; run += v[i].w;
+        st[i] = o;
+        h[i] = uint4_t{0u, 0u, 0u, 0u};
+    }
+}
+
+// Level k's key order: perm[start[key] + rank] = entry, for every entry of the level (grid-stride
+// over its tail). A slot outside the tail, impossible for consistent keys and ranks, is flagged.
+__global__ __launch_bounds__(256) void path_sort_rank(PathParams P) {
+    const int32_t k = P.bounce;
+    const uint32_t n = uint32_t(__builtin_amdgcn_readfirstlane(int(P.ctl[k].tail)));
+    const PathSort so = P.sort;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
+        const uint2_t kr = so.kr[e];
+        const uint32_t dst = so.start[kr.x] + kr.y;
+        if (dst < n) so.perm[dst] = e;
+        else if (P.error_flag) atomicOr(P.error_flag, 2);
+    }
+}
+
 // Occupancy (waves/SIMD) of the two trace kernels, 5..7 (the LDS limit is 7: 22.5 KB per
 // workgroup); tuning path_camera_occ / path_bounce_occ pick another (0 = these defaults). The
 // camera kernel at 7 spills 21 dwords whose write-backs reach HBM (14.9 GB per c4 frame against
 // 4.6 GB at 6) and is no faster.
 constexpr int kCameraOcc = 6;
 constexpr int kBounceOcc = 7;
-template __global__ void path_camera_kernel<false, 5>(PathParams);
-template __global__ void path_camera_kernel<false, 6>(PathParams);
-template __global__ void path_camera_kernel<false, 7>(PathParams);
-template __global__ void path_camera_kernel<true, 4>(PathParams);
-template __global__ void path_bounce_kernel<false, 5>(PathParams);
-template __global__ void path_bounce_kernel<false, 6>(PathParams);
-template __global__ void path_bounce_kernel<false, 7>(PathParams);
-template __global__ void path_bounce_kernel<true, 4>(PathParams);
+#define ATR_PATH_KERNELS(SORT)                                                  \
+    template __global__ void path_camera_kernel<false, 5, SORT>(PathParams);    \
+    template __global__ void path_camera_kernel<false, 6, SORT>(PathParams);    \
+    template __global__ void path_camera_kernel<false, 7, SORT>(PathParams);    \
+    template __global__ void path_camera_kernel<true, 4, SORT>(PathParams);     \
+    template __global__ void path_bounce_kernel<false, 5, SORT>(PathParams);    \
+    template __global__ void path_bounce_kernel<false, 6, SORT>(PathParams);    \
+    template __global__ void path_bounce_kernel<false, 7, SORT>(PathParams);    \
+    template __global__ void path_bounce_kernel<true, 4, SORT>(PathParams);
+ATR_PATH_KERNELS(false)
+ATR_PATH_KERNELS(true)
+#undef ATR_PATH_KERNELS
 
 }  // namespace atr
 
 // ------------------------------------------------------------------ launchers used by capi.cpp
+namespace {
+template <bool SORT>
+void launch_camera(const atr::PathParams& P, int occ, dim3 g, hipStream_t s) {
+    const dim3 b(256);
+    if (P.counters) hipLaunchKernelGGL((atr::path_camera_kernel<true, 4, SORT>), g, b, 0, s, P);
+    else if (occ == 5) hipLaunchKernelGGL((atr::path_camera_kernel<false, 5, SORT>), g, b, 0, s, P);
+    else if (occ == 6) hipLaunchKernelGGL((atr::path_camera_kernel<false, 6, SORT>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((atr::path_camera_kernel<false, 7, SORT>), g, b, 0, s, P);
+}
+template <bool SORT>
+void launch_bounce(const atr::PathParams& P, int occ, dim3 g, hipStream_t s) {
+    const dim3 b(256);
+    if (P.counters) hipLaunchKernelGGL((atr::path_bounce_kernel<true, 4, SORT>), g, b, 0, s, P);
+    else if (occ == 5) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 5, SORT>), g, b, 0, s, P);
+    else if (occ == 6) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 6, SORT>), g, b, 0, s, P);
+    else hipLaunchKernelGGL((atr::path_bounce_kernel<false, 7, SORT>), g, b, 0, s, P);
+}
+}  // namespace
+
+// With P.sort.bits > 0 the launch's survivors go to the staging queue (the queue sort, PathSort).
 extern "C" hipError_t atr_launch_path_camera(const atr::PathParams& P, int occ, hipStream_t s) {
     const int64_t waves = int64_t(P.ncells) * P.cam.samples_per_pixel;
     if (waves <= 0) return hipSuccess;
-    const dim3 g(unsigned((waves + 3) / 4)), b(256);
+    const dim3 g(unsigned((waves + 3) / 4));
     if (!occ) occ = atr::kCameraOcc;
-    if (P.counters) hipLaunchKernelGGL((atr::path_camera_kernel<true, 4>), g, b, 0, s, P);
-    else if (occ == 5) hipLaunchKernelGGL((atr::path_camera_kernel<false, 5>), g, b, 0, s, P);
-    else if (occ == 6) hipLaunchKernelGGL((atr::path_camera_kernel<false, 6>), g, b, 0, s, P);
-    else hipLaunchKernelGGL((atr::path_camera_kernel<false, 7>), g, b, 0, s, P);
+    if (P.sort.bits) launch_camera<true>(P, occ, g, s);
+    else launch_camera<false>(P, occ, g, s);
     return hipGetLastError();
 }
 
 // Persistent: `ncu` x occupancy workgroups (4 waves each, one per SIMD) claim the queue 64 entries
 // at a time.
 extern "C" hipError_t atr_launch_path_bounce(const atr::PathParams& P, int ncu, int occ, hipStream_t s) {
-    const dim3 b(256);
     if (!occ) occ = atr::kBounceOcc;
     const dim3 g(unsigned(ncu) * unsigned(P.counters ? 4 : occ));
-    if (P.counters) hipLaunchKernelGGL((atr::path_bounce_kernel<true, 4>), g, b, 0, s, P);
-    else if (occ == 5) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 5>), g, b, 0, s, P);
-    else if (occ == 6) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 6>), g, b, 0, s, P);
-    else hipLaunchKernelGGL((atr::path_bounce_kernel<false, 7>), g, b, 0, s, P);
+    if (P.sort.bits) launch_bounce<true>(P, occ, g, s);
+    else launch_bounce<false>(P, occ, g, s);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t atr_launch_path_sort(const atr::PathParams& P, int ncu, hipStream_t s) {
+    const unsigned blocks = unsigned(P.sort.nbins / atr::kSortChunk);
+    hipLaunchKernelGGL(atr::path_sort_sums, dim3(blocks), dim3(256), 0, s, P.sort);
+    hipLaunchKernelGGL(atr::path_sort_part_scan, dim3(1), dim3(1024), 0, s, P.sort);
+    hipLaunchKernelGGL(atr::path_sort_scan, dim3(blocks), dim3(256), 0, s, P.sort);
+    hipLaunchKernelGGL(atr::path_sort_rank, dim3(unsigned(ncu) * 16u), dim3(256), 0, s, P);
     return hipGetLastError();
 }
 

@@ -185,10 +185,11 @@ def pmc_counters(args, kernel_name, path_tail=None):
     return out, info, "ok"
 
 
-def path_dispatches(args, tiles, W, H, spp, bounces, batch_log2):
+def path_dispatches(args, tiles, W, H, spp, bounces, batch_log2, sort_bits=0):
     """Kernel dispatches of the path engine in the timed region (capi.cpp launch_paths): per
     launch of nf frames, its nf x blocks cells in batches of 2^batch_log2 / (64 spp) cells; per
-    batch one camera, bounces - 1 bounce and one resolve launch."""
+    batch one camera, bounces - 1 bounce and one resolve launch, and with the queue sort
+    (path_sort_bits) bounces - 1 sorts of four kernels each."""
     cells = set()
     for x0, y0, x1, y1 in tiles:
         for cy in range(max(0, y0) // 8, min(H - 1, y1) // 8 + 1):
@@ -197,7 +198,11 @@ def path_dispatches(args, tiles, W, H, spp, bounces, batch_log2):
     per_batch = max(1, (1 << batch_log2) // (64 * max(1, spp)))
     nb = sum(-(-nf * len(cells) // per_batch) for nf in launch_sizes(args.steps, args.frames_per_launch,
                                                                       max(1, args.streams)))
-    return {"path_camera_kernel": nb, "path_bounce_kernel": nb * max(0, bounces - 1), "path_resolve_kernel": nb}
+    out = {"path_camera_kernel": nb, "path_bounce_kernel": nb * max(0, bounces - 1), "path_resolve_kernel": nb}
+    if sort_bits and bounces >= 2:
+        for k in ("path_sort_sums", "path_sort_part_scan", "path_sort_scan", "path_sort_rank"):
+            out[k] = nb * (bounces - 1)
+    return out
 
 
 def cpu_baseline(asset, W, H, spp, bounces, use_tree, seconds):
@@ -290,7 +295,7 @@ def main():
                     help="diagnostic: raw kernel code passed to the engine (overrides --variant's kernel)")
     ap.add_argument("--tuning", default="",
                     help="diagnostic: k=v,... scheduling knobs for atr_set_tuning (xcd_chunk, frame_rotate, hybrid_a, "
-                         "hybrid_b, path_batch_log2, cluster_size, path_camera_occ, path_bounce_occ, primary_occ); outputs never change")
+                         "hybrid_b, path_batch_log2, cluster_size, path_camera_occ, path_bounce_occ, primary_occ, path_sort_bits); outputs never change")
     ap.add_argument("--side", type=int, default=32,
                     help="shard tile side (pixels); 32 balances the 8-way c3 plan ~4%% better than 64 (DESIGN.md §5)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
@@ -918,10 +923,12 @@ def run(args):
         paths = roof_variant == E.ATR_KERNEL_PATHS
         if world == 1 and not args.no_pmc and paths:
             # the path engine: every kernel of the timed frames (camera, bounces, resolve), per frame
-            tail = path_dispatches(args, tiles_list, W, H, spp, bounces, eng.tuning()["path_batch_log2"])
+            tune = eng.tuning()
+            tail = path_dispatches(args, tiles_list, W, H, spp, bounces, tune["path_batch_log2"], tune["path_sort_bits"])
             pmc, info, why = pmc_counters(args, "path_", tail)
             roof["pmc_note"] = why
-            roof["kernel"] = "path engine: path_camera_kernel + path_bounce_kernel x (bounces - 1) + path_resolve_kernel"
+            roof["kernel"] = ("path engine: path_camera_kernel + path_bounce_kernel x (bounces - 1) + path_resolve_kernel"
+                              + (" + queue sort (path_sort_*) x (bounces - 1)" if len(tail) > 3 else ""))
             if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
                 K = args.steps
                 per_frame = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0 / K

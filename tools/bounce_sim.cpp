@@ -539,7 +539,7 @@ int main(int argc, char** argv) {
     };
     // wave model: rays in generation order, 64 per wave (level 1: a pixel's samples side by side)
     for (int l = 1; l < 3; ++l)
-      for (int order = 0; order < 4; ++order) {
+      for (int order = 0; order < 11; ++order) {
         // 0: queue order; 1: sorted by (origin leaf, direction octant); 2: by direction octant then
         // origin leaf; 3: by a 64-bin direction cell (octant x 8 sub-cells) then origin leaf
         std::vector<RaySeq> R = g_seq[l];
@@ -555,6 +555,41 @@ int main(int argc, char** argv) {
             return oct(a) != oct(b) ? oct(a) < oct(b) : a.oleaf < b.oleaf; });
         if (order == 3) std::stable_sort(R.begin(), R.end(), [&](const RaySeq& a, const RaySeq& b) {
             return cell(a) != cell(b) ? cell(a) < cell(b) : a.oleaf < b.oleaf; });
+        // 4..7: the direction cell, then a Morton code of the origin at 3..6 bits per axis over the
+        // origins' bounding box (what a GPU key can compute without a point location)
+        if (order >= 4) {
+            float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+            for (const auto& r : R)
+                for (int a = 0; a < 3; ++a) lo[a] = std::min(lo[a], r.o[a]), hi[a] = std::max(hi[a], r.o[a]);
+            const int bits = order >= 8 ? 4 : order - 1;
+            auto morton = [&](const RaySeq& r) {
+                uint32_t m = 0;
+                int q[3];
+                for (int a = 0; a < 3; ++a)
+                    q[a] = std::min((1 << bits) - 1, std::max(0, int((r.o[a] - lo[a]) / (hi[a] - lo[a] + 1e-20f) * float(1 << bits))));
+                for (int b = bits - 1; b >= 0; --b)
+                    for (int a = 0; a < 3; ++a) m = (m << 1) | ((q[a] >> b) & 1);
+                return m;
+            };
+            // 8..10: an octahedral direction cell of 8x8, 16x16, 32x32 instead of the 64-bin cell
+            const int oc = order == 8 ? 8 : order == 9 ? 16 : 32;
+            auto ocell = [&](const RaySeq& r) {
+                const float s = std::fabs(r.d[0]) + std::fabs(r.d[1]) + std::fabs(r.d[2]);
+                float u = r.d[0] / s, v = r.d[1] / s;
+                if (r.d[2] < 0) {
+                    const float uu = (1 - std::fabs(v)) * (u >= 0 ? 1 : -1), vv = (1 - std::fabs(u)) * (v >= 0 ? 1 : -1);
+                    u = uu, v = vv;
+                }
+                const int iu = std::min(oc - 1, int((u * 0.5f + 0.5f) * oc)), iv = std::min(oc - 1, int((v * 0.5f + 0.5f) * oc));
+                return iv * oc + iu;
+            };
+            if (order < 8)
+                std::stable_sort(R.begin(), R.end(), [&](const RaySeq& a, const RaySeq& b) {
+                    return cell(a) != cell(b) ? cell(a) < cell(b) : morton(a) < morton(b); });
+            else
+                std::stable_sort(R.begin(), R.end(), [&](const RaySeq& a, const RaySeq& b) {
+                    return ocell(a) != ocell(b) ? ocell(a) < ocell(b) : morton(a) < morton(b); });
+        }
         double k8_iters = 0, k8_steps = 0, lz_iters = 0, lz_steps = 0, waves = 0;
         for (size_t w0 = 0; w0 + 64 <= R.size(); w0 += 64) {
             waves += 1;

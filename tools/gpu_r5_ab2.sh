@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5 A/B, general form: variants "prod", "exp=<name>" (atray_amd/_lib/exp/<name>.so) or
-# "tune=<k=v,...>" (product library, bench.py --tuning), interleaved twice, on the configs given.
+# "tune=<k=v,...>" (product library, bench.py --tuning) or "exp=<name>@<k=v,...>" (both),
+# interleaved twice, on the configs given.
 # usage: gpu_r5_ab2.sh OUTDIR "variant ..." "c3 c4" [tests]
 set -o pipefail
 export TMPDIR=/tmp
@@ -23,6 +24,7 @@ for i in 1 2; do
     n=$((n + 1))
     L=atray_amd/_lib/libatray_hip.so; T=""
     case $v in
+      exp=*@*) x=${v#exp=}; L=atray_amd/_lib/exp/${x%%@*}.so; T="--tuning ${x#*@}";;
       exp=*) L=atray_amd/_lib/exp/${v#exp=}.so;;
       tune=*) T="--tuning ${v#tune=}";;
     esac

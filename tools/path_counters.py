@@ -1,6 +1,7 @@
 """Per-ray work of the path engine by bounce depth (COUNT build; with the diagnostic build, ATRAY_LIB=
 atray_amd/_lib/diag/libatray_hip.so, also the scan phases' wave clocks): c4's camera rays alone
-(bounce_limit 1, spp 64), then bounce limits 2..5 -- each level's rays are the difference."""
+(bounce_limit 1, spp 64), then bounce limits 2..5 -- each level's rays are the difference.
+Environment SORT=b: the queue sort at b bits per axis (tuning path_sort_bits)."""
 import json
 import os
 import sys
@@ -18,6 +19,7 @@ box = m.translate_to(m.aabb(), CENTERS["Dragon"])
 t = E.Octree.build(m, 300)
 eng = E.Engine(0)
 eng.upload(MATERIALS, [(m, t, box, 1)])
+eng.set_tuning(path_sort_bits=int(os.environ.get("SORT", "0")))
 tiles = [[0, 0, W - 1, H - 1]]
 prev = None
 rows = []
