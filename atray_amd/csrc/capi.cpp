@@ -193,6 +193,7 @@ atr_tuning default_tuning() {
     t.path_batch_log2 = 27;  // §4h: 2^27 paths per batch (c4: one batch per frame)
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
     t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs
+    t.path_sort_bits = 6;  // §4h: each level's queue in (direction, origin) order, 6 bits per axis
     return t;
 }
 constexpr int kSchedPaths = 10;             // the sample-parallel path engine (paths.hip)
@@ -234,7 +235,7 @@ struct atr_ctx {
         DevBuf mem;
         int64_t cap = 0;
         int32_t levels = 0;
-        bool sort = false;        // holds the queue-sort buffers (PathSort)
+        int64_t sort_bins = 0;    // queue-sort buffers for this many bins (PathSort), or none
         hipEvent_t ev = nullptr;  // recorded after the latest launch that used `mem`
         uint64_t last_use = 0;
     };
@@ -483,18 +484,18 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
 // launch. So the total stays bounded however many streams render. Growing a workspace waits for
 // its own last launch only. When the device has no memory for it, idle workspaces of other streams
 // are released and the allocation retried once; hipErrorOutOfMemory then goes back to the caller
-// (launch_paths halves its batch, launch_kernels falls back to FLAT).
-// Queue-sort buffers after the queues and counters: {key, rank} and the key order per entry, the
-// bins, their starts and block sums (for kMaxSortBits), 256-B aligned.
+// (launch_paths halves its batch, then drops the queue sort, and launch_kernels falls back to FLAT).
+// Queue-sort buffers after the queues and counters (256-B aligned): {key, rank} and the key order
+// per entry, then `bins` bins, their starts and block sums.
 size_t sort_offset(int64_t cap, int32_t levels) {
     return (size_t(cap) * 16 * (2 * kPathPlanes + 1) + size_t(levels) * sizeof(PathCtl) + 255) & ~size_t(255);
 }
-constexpr int64_t kSortBinsMax = int64_t(64) << (3 * kMaxSortBits);
-size_t sort_bytes(int64_t cap) {
-    return size_t(cap) * 12 + size_t(kSortBinsMax) * 8 + size_t(kSortBinsMax / kSortChunk) * 4;
+size_t sort_bytes(int64_t cap, int64_t bins) {
+    return size_t(cap) * 12 + size_t(bins) * 8 + size_t(bins / kSortChunk) * 4;
 }
 
-hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, bool sort, atr_ctx::PathWS*& out) {
+hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, int64_t sort_bins,
+                          atr_ctx::PathWS*& out) {
     atr_ctx::PathWS* ws = nullptr;
     hipError_t e;
     for (auto& w : c->path_ws)
@@ -515,19 +516,19 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
     if (ws->stream != s && ws->mem.p && (e = hipStreamWaitEvent(s, ws->ev, 0)) != hipSuccess) return e;
     ws->stream = s;
     ws->last_use = ++c->ws_clock;
-    if (ws->cap < cap || ws->levels < levels || (sort && !ws->sort)) {
+    if (ws->cap < cap || ws->levels < levels || ws->sort_bins < sort_bins) {
         if ((e = hipEventSynchronize(ws->ev)) != hipSuccess) return e;
         if (ws->mem.p && (e = hipFree(ws->mem.p)) != hipSuccess) return e;
         ws->mem = DevBuf();
         const int64_t ncap = std::max(ws->cap, cap);
         const int32_t nlev = std::max(ws->levels, levels);
-        const bool nsort = ws->sort || sort;
+        const int64_t nbins = std::max(ws->sort_bins, sort_bins);
         ws->cap = 0;
         ws->levels = 0;
-        ws->sort = false;
+        ws->sort_bins = 0;
         // 2 queues x kPathPlanes planes + the per-path results, 16 B per entry; the level counters;
         // the queue-sort buffers
-        const size_t bytes = nsort ? sort_offset(ncap, nlev) + sort_bytes(ncap)
+        const size_t bytes = nbins ? sort_offset(ncap, nlev) + sort_bytes(ncap, nbins)
                                    : size_t(ncap) * 16 * (2 * kPathPlanes + 1) + size_t(nlev) * sizeof(PathCtl);
         e = hipMalloc(&ws->mem.p, bytes);
         if (e == hipErrorOutOfMemory) {
@@ -538,7 +539,7 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
                     w.mem = DevBuf();
                     w.cap = 0;
                     w.levels = 0;
-                    w.sort = false;
+                    w.sort_bins = 0;
                 }
             e = hipMalloc(&ws->mem.p, bytes);
         }
@@ -550,7 +551,7 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
         ws->mem.n = bytes;
         ws->cap = ncap;
         ws->levels = nlev;
-        ws->sort = nsort;
+        ws->sort_bins = nbins;
     }
     out = ws;
     return hipSuccess;
@@ -567,22 +568,28 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     const int64_t per_cell = 64 * std::max<int64_t>(spp, 1);
     const int32_t levels = std::max(bl, 1);
     // the queue sort pays off only when a level's queue feeds another bounce launch
-    const int32_t sort_bits = bl >= 2 ? c->tune.path_sort_bits : 0;
+    int32_t sort_bits = bl >= 2 ? c->tune.path_sort_bits : 0;
+    while (sort_bits > 0 && (int64_t(kSortDirs) * kSortDirs << (3 * sort_bits)) > kSortBinsMax) --sort_bits;
     atr_ctx::PathWS* ws = nullptr;
     hipError_t e = hipErrorOutOfMemory;
     int64_t cells = 0;
     // a batch of 2^path_batch_log2 paths, halved while the device cannot hold its workspace (down to
-    // 2^16 paths; the outputs do not depend on the batch size)
-    for (int32_t lg = c->tune.path_batch_log2; lg >= 16 && e == hipErrorOutOfMemory; --lg) {
-        const int64_t batch = std::max<int64_t>(1, (int64_t(1) << lg) / per_cell);
-        cells = std::min<int64_t>(batch, P.nblocks);
-        // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
-        // one-frame launch already holds the batch of the multi-frame launches that follow it
-        int64_t cap = 1;
-        while (cap < cells * per_cell) cap <<= 1;
-        cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
-        e = path_workspace(c, s, cap, std::max(levels, 8), sort_bits > 0, ws);
-        if (e == hipSuccess && ws->cap < cap) e = hipErrorOutOfMemory;
+    // 2^16 paths; the outputs do not depend on the batch size); then the same without the queue sort
+    for (;;) {
+        const int64_t bins = sort_bits > 0 ? int64_t(kSortDirs) * kSortDirs << (3 * sort_bits) : 0;
+        for (int32_t lg = c->tune.path_batch_log2; lg >= 16 && e == hipErrorOutOfMemory; --lg) {
+            const int64_t batch = std::max<int64_t>(1, (int64_t(1) << lg) / per_cell);
+            cells = std::min<int64_t>(batch, P.nblocks);
+            // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
+            // one-frame launch already holds the batch of the multi-frame launches that follow it
+            int64_t cap = 1;
+            while (cap < cells * per_cell) cap <<= 1;
+            cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
+            e = path_workspace(c, s, cap, std::max(levels, 8), bins, ws);
+            if (e == hipSuccess && ws->cap < cap) e = hipErrorOutOfMemory;
+        }
+        if (e != hipErrorOutOfMemory || sort_bits == 0) break;
+        sort_bits = 0;
     }
     if (e != hipSuccess) return e;
     PathParams Q;
@@ -618,7 +625,7 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     if (sort_bits > 0) {
         PathSort& so = Q.sort;
         so.bits = sort_bits;
-        so.nbins = int32_t(64) << (3 * sort_bits);
+        so.nbins = int32_t(kSortDirs * kSortDirs) << (3 * sort_bits);
         const float* box = c->scene_box;
         for (int a = 0; a < 3; ++a) {
             so.lo[a] = box[a];
@@ -631,8 +638,8 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
         so.perm = reinterpret_cast<uint32_t*>(sb);
         sb += size_t(ws->cap) * 4;
         so.hist = reinterpret_cast<uint32_t*>(sb);
-        so.start = so.hist + kSortBinsMax;
-        so.part = so.start + kSortBinsMax;
+        so.start = so.hist + ws->sort_bins;
+        so.part = so.start + ws->sort_bins;
     }
     const int occ_cam = c->tune.path_camera_occ, occ_bounce = c->tune.path_bounce_occ;
     for (int64_t c0 = 0; c0 < P.nblocks; c0 += cells) {

@@ -218,18 +218,23 @@ struct PathCtl {
 };
 // Queue sort (tuning path_sort_bits = b > 0): the queues are entry-major (an entry's
 // four records together, q[4 e + i], 64 B) and every queued path also records {key, rank} in `kr`:
-// key = the ray's direction cell (octant x dominant axis x steep, 6 bits) above a Morton code of its
-// origin quantised to b bits per axis over the scene box (lo, sc = 2^b / extent), rank = its arrival
+// key = the ray's direction cell (kSortDirs^2 octahedral cells) above a Morton code of its origin
+// quantised to b bits per axis over the scene box (lo, sc = 2^b / extent), rank = its arrival
 // in the key's bin (atomicAdd on hist). The sort launches turn hist into bin starts and write the
 // level's key order perm[start[key] + rank] = entry; the next bounce launch's waves claim positions
 // of that order, so a wavefront takes rays of one direction cell and one region together (a
 // counting sort of 4-B indices; the entries never move; the order within a bin is arrival order,
 // and no output depends on queue order).
+#ifndef ATR_SORT_DIRS
+#define ATR_SORT_DIRS 8
+#endif
+constexpr int kSortDirs = ATR_SORT_DIRS;  // direction cells per side of the octahedral map
 constexpr int kMaxSortBits = 7;
+constexpr int64_t kSortBinsMax = int64_t(1) << 27;  // 64 direction cells x 7 bits per axis
 constexpr int32_t kSortChunk = 4096;  // bins per block of the bin scan
 struct PathSort {
     int32_t bits;      // 0: off
-    int32_t nbins;     // 64 << 3 bits
+    int32_t nbins;     // kSortDirs^2 << 3 bits
     float lo[3], sc[3];
     uint2_t* kr;       // {key, rank} per entry of the level being written
     uint32_t* perm;    // the previous level's key order (entry per position)

@@ -22,9 +22,6 @@
 
 #include "scan.h"
 
-#ifndef ATR_SORT_KEY
-#define ATR_SORT_KEY 0
-#endif
 
 namespace atr {
 
@@ -52,46 +49,34 @@ __device__ __forceinline__ void path_finish(float4_t* out, uint32_t o, V3 ret, u
     out[o] = float4_t{ret.x, ret.y, ret.z, __uint_as_float(casts)};
 }
 
-// Sort key of a queued ray (PathSort, engine.h): direction cell (octant, dominant axis, |d| of that
-// axis above 0.85) above the Morton code of its origin's cell, b bits per axis over the scene box.
+// Sort key of a queued ray (PathSort, engine.h): the octahedral cell of its direction (kSortDirs x
+// kSortDirs over the unfolded octahedron) above the Morton code of its origin's cell, b bits per axis
+// over the scene box.
 __device__ __forceinline__ uint32_t spread3(uint32_t x) {  // bits 0..9 -> every third bit
     x = (x | (x << 16)) & 0x030000FFu;
     x = (x | (x << 8)) & 0x0300F00Fu;
     x = (x | (x << 4)) & 0x030C30C3u;
     return (x | (x << 2)) & 0x09249249u;
 }
-__device__ __forceinline__ uint32_t path_sort_morton(V3 o, PathSort so) {
+__device__ __forceinline__ uint32_t path_sort_key(V3 o, V3 d, PathSort so) {
     const float qmax = float((1 << so.bits) - 1);
     // fmaxf first: a NaN coordinate lands in cell 0
     const uint32_t qx = uint32_t(fminf(fmaxf((o.x - so.lo[0]) * so.sc[0], 0.0f), qmax));
     const uint32_t qy = uint32_t(fminf(fmaxf((o.y - so.lo[1]) * so.sc[1], 0.0f), qmax));
     const uint32_t qz = uint32_t(fminf(fmaxf((o.z - so.lo[2]) * so.sc[2], 0.0f), qmax));
-    return (spread3(qx) << 2) | (spread3(qy) << 1) | spread3(qz);
-}
-__device__ __forceinline__ uint32_t path_sort_key(V3 o, V3 d, PathSort so) {
-    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-    const uint32_t oct = (d.x < 0.0f ? 4u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 1u : 0u);
-    const uint32_t major = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
-    const uint32_t steep = fmaxf(ax, fmaxf(ay, az)) > 0.85f ? 1u : 0u;
-#if ATR_SORT_KEY == 2  // experiment: an octahedral 8 x 8 direction cell
-    {
-        const float sum = ax + ay + az;
-        float u = d.x / sum, v = d.y / sum;
-        if (d.z < 0.0f) {
-            const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
-            v = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
-            u = uu;
-        }
-        const uint32_t iu = uint32_t(fminf(fmaxf((u * 0.5f + 0.5f) * 8.0f, 0.0f), 7.0f));
-        const uint32_t iv = uint32_t(fminf(fmaxf((v * 0.5f + 0.5f) * 8.0f, 0.0f), 7.0f));
-        (void)oct, (void)major, (void)steep;
-        return ((iv * 8u + iu) << (3 * so.bits)) | path_sort_morton(o, so);
+    const uint32_t morton = (spread3(qx) << 2) | (spread3(qy) << 1) | spread3(qz);
+    // octahedral direction: (x, y) / (|x| + |y| + |z|), the lower hemisphere folded out
+    const float sum = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float u = d.x / sum, v = d.y / sum;
+    if (d.z < 0.0f) {
+        const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+        v = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+        u = uu;
     }
-#elif ATR_SORT_KEY == 1  // experiment: origin cell above the direction cell
-    return (path_sort_morton(o, so) << 6) | (oct << 3) | (major << 1) | steep;
-#else
-    return (((oct << 3) | (major << 1) | steep) << (3 * so.bits)) | path_sort_morton(o, so);
-#endif
+    constexpr float D = float(kSortDirs);
+    const uint32_t iu = uint32_t(fminf(fmaxf((u * 0.5f + 0.5f) * D, 0.0f), D - 1.0f));
+    const uint32_t iv = uint32_t(fminf(fmaxf((v * 0.5f + 0.5f) * D, 0.0f), D - 1.0f));
+    return ((iv * uint32_t(kSortDirs) + iu) << (3 * so.bits)) | morton;
 }
 
 // Append this lane's path (if `go`) to queue q (planes `cap` entries apart): one atomic per wave for

@@ -181,7 +181,7 @@ typedef struct {
     int32_t path_sort_bits; /* PATHS: 2..7 = each level's queue is sorted by (direction cell,
                                origin cell with this many bits per axis of the scene box) before
                                the next bounce launch, so a wavefront takes rays that walk the same
-                               tree nodes; 0 = queue order */
+                               tree nodes; 0 = queue order; default 6 */
     int32_t reserved[1];    /* must be 0 */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
