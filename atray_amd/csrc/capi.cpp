@@ -193,7 +193,7 @@ atr_tuning default_tuning() {
     t.path_batch_log2 = 27;  // §4h: 2^27 paths per batch (c4: one batch per frame)
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
     t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs
-    t.path_sort_bits = 6;  // §4h: each level's queue in (direction, origin) order, 6 bits per axis
+    t.path_sort_bits = 5;  // §4h: each level's queue in (direction, origin) order, 5 bits per axis
     return t;
 }
 constexpr int kSchedPaths = 10;             // the sample-parallel path engine (paths.hip)

@@ -226,11 +226,11 @@ struct PathCtl {
 // counting sort of 4-B indices; the entries never move; the order within a bin is arrival order,
 // and no output depends on queue order).
 #ifndef ATR_SORT_DIRS
-#define ATR_SORT_DIRS 8
+#define ATR_SORT_DIRS 16
 #endif
 constexpr int kSortDirs = ATR_SORT_DIRS;  // direction cells per side of the octahedral map
 constexpr int kMaxSortBits = 7;
-constexpr int64_t kSortBinsMax = int64_t(1) << 27;  // 64 direction cells x 7 bits per axis
+constexpr int64_t kSortBinsMax = int64_t(1) << 26;  // 256 direction cells x 6 bits per axis
 constexpr int32_t kSortChunk = 4096;  // bins per block of the bin scan
 struct PathSort {
     int32_t bits;      // 0: off

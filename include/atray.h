@@ -178,10 +178,11 @@ typedef struct {
     int32_t primary_occ;    /* HYBRID primary cell launches: waves/SIMD 6, 7 or 8, or 0 = the
                                measured default (8 for one frame, 7 for frames in flight;
                                DESIGN.md §4e) */
-    int32_t path_sort_bits; /* PATHS: 2..7 = each level's queue is sorted by (direction cell,
-                               origin cell with this many bits per axis of the scene box) before
-                               the next bounce launch, so a wavefront takes rays that walk the same
-                               tree nodes; 0 = queue order; default 6 */
+    int32_t path_sort_bits; /* PATHS: 2..7 = each level's queue is put in the order of (the ray's
+                               direction cell, 16 x 16 octahedral; its origin's cell, this many
+                               bits per axis of the scene box) before the next bounce launch, so a
+                               wavefront takes rays that walk the same tree nodes (6 at most is
+                               used); 0 = queue order; default 5 */
     int32_t reserved[1];    /* must be 0 */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);

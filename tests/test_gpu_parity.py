@@ -287,7 +287,7 @@ def test_tuning_changes_no_output(eng, variant):
     settings = [{"xcd_chunk": 0}, {"xcd_chunk": 3}, {"hybrid_a": -4096, "hybrid_b": -4096},
                 {"hybrid_a": 4096, "hybrid_b": 4096}, {"path_batch_log2": 12}, {"cluster_size": 7},
                 {"frame_plan": 0}, {"primary_occ": 7}, {"primary_occ": 8}, {"path_camera_occ": 5, "path_bounce_occ": 6},
-                {"path_camera_occ": 7}, {"path_sort_bits": 0}, {"path_sort_bits": 4},
+                {"path_camera_occ": 7}, {"path_sort_bits": 0}, {"path_sort_bits": 4}, {"path_sort_bits": 7},
                 {"path_sort_bits": 2, "path_batch_log2": 12}, {"path_sort_bits": 5, "path_bounce_occ": 5}]
     try:
         for spp, bounces in ((1, 1), (2, 3)):
