@@ -183,6 +183,9 @@ int32_t default_parse_threads() {
     const unsigned hw = std::thread::hardware_concurrency();
     return int32_t(std::max(1u, std::min(16u, hw)));
 }
+#ifndef ATR_PATH_SPLIT_DEFAULT
+#define ATR_PATH_SPLIT_DEFAULT 0
+#endif
 atr_tuning default_tuning() {
     atr_tuning t;
     std::memset(&t, 0, sizeof(t));
@@ -194,6 +197,7 @@ atr_tuning default_tuning() {
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
     t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs
     t.path_sort_bits = 5;  // §4h: each level's queue in (direction, origin) order, 5 bits per axis
+    t.path_split = ATR_PATH_SPLIT_DEFAULT;  // §4h: a one-batch launch as two half batches
     return t;
 }
 constexpr int kSchedPaths = 10;             // the sample-parallel path engine (paths.hip)
@@ -240,6 +244,9 @@ struct atr_ctx {
         uint64_t last_use = 0;
     };
     static constexpr size_t kMaxPathWS = 4;  // workspaces at most (streams beyond share them)
+    // a one-batch PATHS launch runs as two half batches on these streams (fork / join events)
+    hipStream_t split_stream[2] = {};
+    hipEvent_t split_fork = nullptr, split_join[2] = {};
     uint64_t ws_clock = 0;
     std::vector<PathWS> path_ws;
     // launches' traced-ray counter sets: a ring, each set reused only after the launch that last
@@ -560,10 +567,10 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
 // The sample-parallel path engine (paths.hip) over a cell launch's blocks: the cell list in
 // batches of 2^tuning.path_batch_log2 paths, per batch the camera launch, one launch per further
 // bounce (persistent waves over the previous level's queue) and the per-pixel resolve, all on s.
-hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
+hipError_t launch_paths_range(atr_ctx* c, const RenderParams& P, hipStream_t s, int64_t cbeg, int64_t cend) {
     const int64_t spp = P.cam.samples_per_pixel;
     const int32_t bl = P.cam.bounce_limit;
-    if (P.nblocks <= 0) return hipSuccess;
+    if (cend <= cbeg) return hipSuccess;
     if (bl > kMaxPathBounces) return hipErrorInvalidValue;
     const int64_t per_cell = 64 * std::max<int64_t>(spp, 1);
     const int32_t levels = std::max(bl, 1);
@@ -579,7 +586,7 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
         const int64_t bins = sort_bits > 0 ? int64_t(kSortDirs) * kSortDirs << (3 * sort_bits) : 0;
         for (int32_t lg = c->tune.path_batch_log2; lg >= 16 && e == hipErrorOutOfMemory; --lg) {
             const int64_t batch = std::max<int64_t>(1, (int64_t(1) << lg) / per_cell);
-            cells = std::min<int64_t>(batch, P.nblocks);
+            cells = std::min<int64_t>(batch, cend - cbeg);
             // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
             // one-frame launch already holds the batch of the multi-frame launches that follow it
             int64_t cap = 1;
@@ -642,9 +649,9 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
         so.part = so.start + ws->sort_bins;
     }
     const int occ_cam = c->tune.path_camera_occ, occ_bounce = c->tune.path_bounce_occ;
-    for (int64_t c0 = 0; c0 < P.nblocks; c0 += cells) {
+    for (int64_t c0 = cbeg; c0 < cend; c0 += cells) {
         Q.cell0 = int32_t(c0);
-        Q.ncells = int32_t(std::min<int64_t>(cells, P.nblocks - c0));
+        Q.ncells = int32_t(std::min<int64_t>(cells, cend - c0));
         if (bl > 0 && spp > 0) {
             if ((e = hipMemsetAsync(Q.ctl, 0, sizeof(PathCtl) * size_t(levels), s)) != hipSuccess) return e;
             if (sort_bits > 0 &&
@@ -663,6 +670,39 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
         if ((e = atr_launch_path_resolve(Q, s)) != hipSuccess) return e;
     }
     return hipEventRecord(ws->ev, s);
+}
+
+// The path engine over a launch's cell list. A launch that is one batch (a single frame, c4's
+// 2 M-pixel frame at 64 spp) runs as two half batches on the context's two split streams, forked
+// from and joined back into s, so one half's level tails and queue sorts overlap the other half's
+// tracing (tuning path_split; outputs do not depend on the batching).
+constexpr int64_t kSplitMinCells = 1024;
+hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
+    if (P.nblocks <= 0) return hipSuccess;
+    const int64_t per_cell = 64 * std::max<int64_t>(P.cam.samples_per_pixel, 1);
+    const int64_t batch = std::max<int64_t>(1, (int64_t(1) << c->tune.path_batch_log2) / per_cell);
+    if (!c->tune.path_split || P.nblocks > batch || P.nblocks < kSplitMinCells || P.counters || P.block_cost)
+        return launch_paths_range(c, P, s, 0, P.nblocks);
+    hipError_t e;
+    if (!c->split_fork) {
+        for (int i = 0; i < 2; ++i) {
+            if ((e = hipStreamCreateWithFlags(&c->split_stream[i], hipStreamNonBlocking)) != hipSuccess) return e;
+            if ((e = hipEventCreateWithFlags(&c->split_join[i], hipEventDisableTiming)) != hipSuccess) return e;
+        }
+        if ((e = hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    if ((e = hipEventRecord(c->split_fork, s)) != hipSuccess) return e;
+    const int64_t half = (P.nblocks + 1) / 2;
+    hipError_t r = hipSuccess;
+    for (int i = 0; i < 2; ++i) {
+        hipStream_t a = c->split_stream[i];
+        if ((e = hipStreamWaitEvent(a, c->split_fork, 0)) != hipSuccess) return e;
+        if (r == hipSuccess) r = launch_paths_range(c, P, a, i ? half : 0, i ? P.nblocks : half);
+        // joined whatever happened, so a fallback render on s runs after anything queued here
+        if ((e = hipEventRecord(c->split_join[i], a)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, c->split_join[i], 0)) != hipSuccess) return e;
+    }
+    return r;
 }
 
 hipError_t launch_kernels(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
@@ -977,10 +1017,9 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
         t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
         (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)) ||
         (t->primary_occ != 0 && (t->primary_occ < 6 || t->primary_occ > 8)) ||
-        (t->path_sort_bits != 0 && (t->path_sort_bits < 2 || t->path_sort_bits > kMaxSortBits)))
+        (t->path_sort_bits != 0 && (t->path_sort_bits < 2 || t->path_sort_bits > kMaxSortBits)) ||
+        t->path_split < 0 || t->path_split > 1)
         return ATR_E_INVALID;
-    for (int32_t r : t->reserved)
-        if (r) return ATR_E_INVALID;
     c->tune = *t;
     return ATR_OK;
 }
@@ -1021,6 +1060,11 @@ int atr_destroy(atr_ctx* c) {
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    for (int i = 0; i < 2; ++i) {
+        if (c->split_stream[i]) (void)hipStreamDestroy(c->split_stream[i]);
+        if (c->split_join[i]) (void)hipEventDestroy(c->split_join[i]);
+    }
+    if (c->split_fork) (void)hipEventDestroy(c->split_fork);
     delete c;
     return ATR_OK;
 }

@@ -305,7 +305,11 @@ def main():
     ap.add_argument("--no-steady", action="store_true",
                     help="skip the steady-state figure (64 further frames in 16-frame launches, after the timed region)")
     ap.add_argument("--no-orbit", action="store_true", help="every frame from the app camera")
-    ap.add_argument("--streams", type=int, default=2, help="launches in flight (one HIP stream each)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="launches in flight (one HIP stream each); 0 = 2 for the 1-spp configs (c1-c3: one "
+                         "launch's tail hides behind the other's work) and 1 for the path-engine configs (c4, c5: "
+                         "two concurrent launches share the caches that the sorted bounce queues rely on, "
+                         "DESIGN.md §4h)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch; "
                          "0 = the K steps in as few launches per stream as the cap allows, at least 4 x ranks "
@@ -353,6 +357,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.streams <= 0:
+        spp, bounces = CONFIGS[args.config][3:5]
+        args.streams = 1 if (spp > 1 or bounces > 1) else 2
     if args.frames_per_launch <= 0:
         args.frames_per_launch = max(4 * max(world, args.sim_world), -(-args.steps // max(1, args.streams)))
     args.frames_per_launch = max(1, min(16, args.frames_per_launch))

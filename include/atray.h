@@ -154,7 +154,7 @@ const char* atr_version(void);
 /* Scheduling knobs of a context. They change launch order and work distribution only, never an
    output bit (every value is covered by the GPU parity tests). atr_default_tuning fills the
    measured defaults; atr_set_tuning validates and copies (ATR_E_INVALID on an out
-   of range field or a nonzero reserved word); cluster_size takes effect at the next
+   of range field); cluster_size takes effect at the next
    atr_scene_upload, the others at the next launch. */
 typedef struct {
     int32_t xcd_chunk;      /* cell schedules: consecutive workgroups per XCD chunk (0 = one
@@ -183,7 +183,9 @@ typedef struct {
                                bits per axis of the scene box) before the next bounce launch, so a
                                wavefront takes rays that walk the same tree nodes (6 at most is
                                used); 0 = queue order; default 5 */
-    int32_t reserved[1];    /* must be 0 */
+    int32_t path_split;     /* PATHS: 1 = a launch that is one batch (a single frame) runs as two
+                               half batches on two internal streams, forked from and joined back
+                               into the render's stream; 0 = one stream */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
 int atr_set_tuning(atr_ctx* ctx, const atr_tuning* tuning);

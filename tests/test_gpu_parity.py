@@ -280,14 +280,16 @@ def test_cell_plan_under_frame_plan_changes_no_output(eng, variant):
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_tuning_changes_no_output(eng, variant):
     """atr_set_tuning: XCD chunking, the HYBRID deal rule forced to always / never deal, the path
-    engine's batch size (2^12 paths: dozens of batches per frame), occupancies and queue sort,
+    engine's batch size (2^12 paths: dozens of batches per frame), occupancies, queue sort and the
+    two-stream split of one-batch launches,
     the HYBRID primary's occupancy and the cluster size (re-upload) change scheduling only -- every output identical, primary and multi-bounce."""
     W, H = 480, 270
     base = eng.tuning()
     settings = [{"xcd_chunk": 0}, {"xcd_chunk": 3}, {"hybrid_a": -4096, "hybrid_b": -4096},
                 {"hybrid_a": 4096, "hybrid_b": 4096}, {"path_batch_log2": 12}, {"cluster_size": 7},
                 {"frame_plan": 0}, {"primary_occ": 7}, {"primary_occ": 8}, {"path_camera_occ": 5, "path_bounce_occ": 6},
-                {"path_camera_occ": 7}, {"path_sort_bits": 0}, {"path_sort_bits": 4}, {"path_sort_bits": 7},
+                {"path_camera_occ": 7}, {"path_sort_bits": 0}, {"path_sort_bits": 4}, {"path_sort_bits": 7}, {"path_split": 1},
+                {"path_split": 1, "path_sort_bits": 0},
                 {"path_sort_bits": 2, "path_batch_log2": 12}, {"path_sort_bits": 5, "path_bounce_occ": 5}]
     try:
         for spp, bounces in ((1, 1), (2, 3)):
@@ -314,6 +316,8 @@ def test_tuning_changes_no_output(eng, variant):
     for bits in (1, 8, -1):
         with pytest.raises(E.AtrError):
             eng.set_tuning(path_sort_bits=bits)
+    with pytest.raises(E.AtrError):
+        eng.set_tuning(path_split=2)
     assert eng.tuning() == base
 
 

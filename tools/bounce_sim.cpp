@@ -99,7 +99,7 @@ int g_level = 0;
 int g_min_safe = 1;  // lazy_restart: safe leaves a pass returns at least (argv[4])
 // per traced ray of the current level, for the wave model: the kernel's passes (visits, leaves
 // consumed) and the lazy walk's visits before each leaf it scans
-struct RaySeq { std::vector<std::pair<int, int>> k8; std::vector<int> lazy; float o[3], d[3]; int oleaf = -1; };
+struct RaySeq { std::vector<std::pair<int, int>> k8; std::vector<int> lazy; std::vector<int32_t> p1; float o[3], d[3]; int oleaf = -1; };
 std::vector<RaySeq> g_seq[3];
 
 // Inner-node visits of three traversal schedules for the same query (the leaf set and order are the
@@ -420,6 +420,7 @@ void walk_model(const Scene& S, V3 o, V3 d, int improving, const std::vector<std
                     continue;
                 }
                 visits += 1;
+                if (passes.empty()) g_seq[g_level].back().p1.push_back(p.node);  // first pass's nodes
                 Examined e = examine(S, o, inv, p.node);
                 for (auto& lf : e.leaves) {
                     if (!lex_less(bd, bi, lf.first, lf.second)) continue;  // at or before the re-walk bound
@@ -591,8 +592,32 @@ int main(int argc, char** argv) {
                     return ocell(a) != ocell(b) ? ocell(a) < ocell(b) : morton(a) < morton(b); });
         }
         double k8_iters = 0, k8_steps = 0, lz_iters = 0, lz_steps = 0, waves = 0;
+        double p1_max = 0, p1_mean = 0, p1_union = 0, p1_uniform = 0;
         for (size_t w0 = 0; w0 + 64 <= R.size(); w0 += 64) {
             waves += 1;
+            {   // first passes: per-lane walks (wave iterations = the longest) vs one wave-walked
+                // near-first pass for a common direction-sign octant (iterations = the union)
+                std::vector<int32_t> all;
+                size_t mx = 0, sum = 0, n = 0;
+                int sm0 = -1;
+                bool uni = true;
+                for (int i = 0; i < 64; ++i) {
+                    const auto& v = R[w0 + i].p1;
+                    if (v.empty()) continue;
+                    const int sm = (R[w0 + i].d[0] < 0) * 4 + (R[w0 + i].d[1] < 0) * 2 + (R[w0 + i].d[2] < 0);
+                    if (sm0 < 0) sm0 = sm;
+                    uni = uni && sm == sm0;
+                    mx = std::max(mx, v.size());
+                    sum += v.size();
+                    ++n;
+                    all.insert(all.end(), v.begin(), v.end());
+                }
+                std::sort(all.begin(), all.end());
+                p1_union += double(std::unique(all.begin(), all.end()) - all.begin());
+                p1_max += double(mx);
+                p1_mean += n ? double(sum) / double(n) : 0.0;
+                p1_uniform += uni ? 1.0 : 0.0;
+            }
             {   // the kernel: a pass phase whenever a lane needs a pass (all lanes wait), then a leaf step
                 std::vector<size_t> p(64, 0);
                 std::vector<int> c(64, 0);
@@ -631,8 +656,10 @@ int main(int argc, char** argv) {
                 }
             }
         }
-        std::printf("level %d order %d wave model (%.0f waves): DFS wave iterations %.1f -> %.1f lazy; leaf steps %.1f -> %.1f\n",
-                    l, order, waves, k8_iters / waves, lz_iters / waves, k8_steps / waves, lz_steps / waves);
+        std::printf("level %d order %d wave model (%.0f waves): DFS wave iterations %.1f -> %.1f lazy; leaf steps %.1f -> %.1f;"
+                    " first pass nodes: lane mean %.1f, wave max %.1f, wave union %.1f, one octant %.2f\n",
+                    l, order, waves, k8_iters / waves, lz_iters / waves, k8_steps / waves, lz_steps / waves,
+                    p1_mean / waves, p1_max / waves, p1_union / waves, p1_uniform / waves);
     }
     for (int l = 0; l < 3; ++l) {
         const Walk& w = g_walk[l];

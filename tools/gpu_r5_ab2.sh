@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5 A/B, general form: variants "prod", "exp=<name>" (atray_amd/_lib/exp/<name>.so) or
-# "tune=<k=v,...>" (product library, bench.py --tuning) or "exp=<name>@<k=v,...>" (both),
+# "tune=<k=v,...>" (product library, bench.py --tuning), "exp=<name>@<k=v,...>" (both) or
+# "args=<arg>+<arg>..." (product library, these bench.py arguments, e.g. args=--streams=1),
 # interleaved twice, on the configs given.
 # usage: gpu_r5_ab2.sh OUTDIR "variant ..." "c3 c4" [tests]
 set -o pipefail
@@ -27,6 +28,7 @@ for i in 1 2; do
       exp=*@*) x=${v#exp=}; L=atray_amd/_lib/exp/${x%%@*}.so; T="--tuning ${x#*@}";;
       exp=*) L=atray_amd/_lib/exp/${v#exp=}.so;;
       tune=*) T="--tuning ${v#tune=}";;
+      args=*) T=$(echo ${v#args=} | tr '+' ' ');;
     esac
     for cfg in $3; do
       case $cfg in
