@@ -72,7 +72,8 @@ def collect_final(d):
     import shutil
     import subprocess
     G = os.path.join(R, "gpurun_out")
-    verify = {}
+    vpath = f"{P}/verify_r05.json"
+    verify = json.load(open(vpath)) if os.path.exists(vpath) else {}  # configs not in d keep theirs
     for cfg in ("c3", "c4", "c5"):
         src = os.path.join(d, f"bench_{cfg}.json")
         if not os.path.exists(src):
