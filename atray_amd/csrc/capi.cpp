@@ -193,7 +193,7 @@ atr_tuning default_tuning() {
     t.frame_rotate = 0;    // §4b: rotation measured slower
     t.hybrid_a = 2;        // §4e: sweep optimum
     t.hybrid_b = 0;
-    t.path_batch_log2 = 27;  // §4h: 2^27 paths per batch (c4: one batch per frame)
+    t.path_batch_log2 = 28;  // §4h: 2^28 paths per batch (c4: a frame in one batch, two per batch in flight)
     t.cluster_size = kMaxClusterSize;  // §4b: 8-16 is the flat optimum
     t.frame_plan = 1;      // §4g: single-frame launches dispatch by the previous frame's costs
     t.path_sort_bits = 5;  // §4h: each level's queue in (direction, origin) order, 5 bits per axis

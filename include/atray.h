@@ -164,8 +164,9 @@ typedef struct {
     int32_t hybrid_a, hybrid_b; /* HYBRID: a leaf step is dealt over the lanes when the largest
                                cluster count exceeds a x rounds + b, -4096..4096; default 2, 0 */
     int32_t path_batch_log2; /* PATHS: paths per batch = 2^this (the path queues hold one batch,
-                               144 B per path), 12..28; default 27 (1920x1080 at 64 spp: one
-                               batch per frame). 2^29 measured 5-7x slower */
+                               144 B per path, 156 with the queue sort), 12..28; default 28
+                               (1920x1080 at 64 spp: a frame in one batch). 2^29 measured 5-7x
+                               slower */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
     int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
                                dispatches its tiles' cells by that launch's measured cost, heaviest

@@ -221,6 +221,6 @@ def test_default_tuning_is_the_measured_schedule():
     t = E.atr_tuning()
     E.lib().atr_default_tuning(C.byref(t))
     got = {f: getattr(t, f) for f, _ in E.atr_tuning._fields_ if f != "reserved"}
-    assert got == {"xcd_chunk": 16, "frame_rotate": 0, "hybrid_a": 2, "hybrid_b": 0, "path_batch_log2": 27,
+    assert got == {"xcd_chunk": 16, "frame_rotate": 0, "hybrid_a": 2, "hybrid_b": 0, "path_batch_log2": 28,
                    "cluster_size": 16, "frame_plan": 1, "path_camera_occ": 0, "path_bounce_occ": 0,
                    "primary_occ": 0, "path_sort_bits": 5, "path_split": 0}
