@@ -409,11 +409,27 @@ __global__ __launch_bounds__(256) void path_sort_rank(PathParams P) {
     const int32_t k = P.bounce;
     const uint32_t n = uint32_t(__builtin_amdgcn_readfirstlane(int(P.ctl[k].tail)));
     const PathSort so = P.sort;
-    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
-        const uint2_t kr = so.kr[e];
-        const uint32_t dst = so.start[kr.x] + kr.y;
-        if (dst < n) so.perm[dst] = e;
-        else if (P.error_flag) atomicOr(P.error_flag, 2);
+    // four entries per lane per step: their loads in flight together (c4 +0.2% over one)
+    constexpr int U = 4;
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t e0 = blockIdx.x * 256u + threadIdx.x; e0 < n; e0 += U * stride) {
+        uint2_t kr[U];
+        uint32_t st[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t e = e0 + uint32_t(j) * stride;
+            kr[j] = e < n ? so.kr[e] : uint2_t{0u, 0u};
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) st[j] = so.start[kr[j].x];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t e = e0 + uint32_t(j) * stride;
+            const uint32_t dst = st[j] + kr[j].y;
+            if (e >= n) continue;
+            if (dst < n) so.perm[dst] = e;
+            else if (P.error_flag) atomicOr(P.error_flag, 2);
+        }
     }
 }
 
