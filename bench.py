@@ -63,6 +63,14 @@ GOLDEN_COUNTERS = {"c3": "dragon_1920x1080_tree", "c2": "monkey_1280x720_bf", "c
 MATERIALS = [((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)]  # app.cpp:91-105
 
 
+def default_streams(config):
+    """Launches in flight by default: two for the 1-spp configs (one launch's tail hides behind the
+    other's work), one for the path-engine configs (two concurrent launches share the caches the
+    sorted bounce queues rely on)."""
+    spp, bounces = CONFIGS[config][3:5]
+    return 1 if (spp > 1 or bounces > 1) else 2
+
+
 def orbit_eye(k):
     a = 2.0 * math.pi * (k % ORBIT_PERIOD) / ORBIT_PERIOD
     return (APP_EYE[0] + ORBIT_RADIUS * math.sin(a), APP_EYE[1], APP_EYE[2] + ORBIT_RADIUS * (1.0 - math.cos(a)))
@@ -358,8 +366,7 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.streams <= 0:
-        spp, bounces = CONFIGS[args.config][3:5]
-        args.streams = 1 if (spp > 1 or bounces > 1) else 2
+        args.streams = default_streams(args.config)
     if args.frames_per_launch <= 0:
         args.frames_per_launch = max(4 * max(world, args.sim_world), -(-args.steps // max(1, args.streams)))
     args.frames_per_launch = max(1, min(16, args.frames_per_launch))

@@ -61,3 +61,24 @@ def test_orbit_cameras_are_distinct():
     eyes = {bench.orbit_eye(k) for k in range(bench.ORBIT_PERIOD)}
     assert len(eyes) == bench.ORBIT_PERIOD
     assert bench.orbit_eye(0) == bench.APP_EYE
+
+
+def test_path_dispatches_count_the_queue_sort():
+    """The PMC selection of the path engine's timed dispatches (bench.path_dispatches): per batch one
+    camera, bounces - 1 bounce and one resolve launch, and with the queue sort four sort kernels
+    per bounce launch; a c4 launch of 8 frames at 2^28-path batches is 4 batches."""
+    class A:
+        steps, frames_per_launch, streams = 8, 8, 1
+    tiles = [[0, 0, 1919, 1079]]
+    d = bench.path_dispatches(A, tiles, 1920, 1080, 64, 5, 28, sort_bits=5)
+    assert d["path_camera_kernel"] == 4 and d["path_bounce_kernel"] == 16 and d["path_resolve_kernel"] == 4
+    for k in ("path_sort_sums", "path_sort_part_scan", "path_sort_scan", "path_sort_rank"):
+        assert d[k] == 16
+    d0 = bench.path_dispatches(A, tiles, 1920, 1080, 64, 5, 28, sort_bits=0)
+    assert set(d0) == {"path_camera_kernel", "path_bounce_kernel", "path_resolve_kernel"}
+    assert bench.path_dispatches(A, tiles, 1920, 1080, 64, 1, 28, sort_bits=5).keys() == d0.keys()
+
+
+def test_streams_default_per_config():
+    """bench.py --streams 0 (default): two for the 1-spp configs, one for the path-engine configs."""
+    assert {c: bench.default_streams(c) for c in bench.CONFIGS} == {"c1": 2, "c2": 2, "c3": 2, "c4": 1, "c5": 1}

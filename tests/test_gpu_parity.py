@@ -321,6 +321,33 @@ def test_tuning_changes_no_output(eng, variant):
     assert eng.tuning() == base
 
 
+def test_queue_sort_at_scale(eng):
+    """The path engine's queue sort at a c4-like shape -- 960x540 at 16 spp, 5
+    bounces: 8.3 M paths, ~2 M per bounce level over the 2^23 bins -- in one batch and in 2^20-path
+    batches (a sort per level per batch), at the default and the largest key: every output and the
+    traced-ray count identical to queue order; framebuffer, hit records and ray counts also equal
+    FLAT's (the cell megakernel)."""
+    upload(eng, "Dragon", True)
+    cam = E.camera(960, 540, 16, 5)
+    base = eng.tuning()
+    try:
+        flat = run(eng, cam, variant=E.ATR_KERNEL_FLAT)
+        eng.set_tuning(path_sort_bits=0)
+        want = run(eng, cam, variant=E.ATR_KERNEL_PATHS)
+        for k in ("fb", "face", "t", "casts"):
+            assert np.array_equal(flat[k].view(np.uint32), want[k].view(np.uint32)), k
+        for kw in ({"path_sort_bits": base["path_sort_bits"]}, {"path_sort_bits": 6},
+                   {"path_sort_bits": base["path_sort_bits"], "path_batch_log2": 20}):
+            eng.set_tuning(**kw)
+            got = run(eng, cam, variant=E.ATR_KERNEL_PATHS)
+            eng.set_tuning(**base)
+            for k in ("fb", "face", "t", "casts", "rgb"):
+                assert np.array_equal(want[k].view(np.uint32), got[k].view(np.uint32)), (kw, k)
+            assert want["traced"] == got["traced"], kw
+    finally:
+        eng.set_tuning(**base)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_frame_plan_changes_no_output(eng, variant):
     """The single-frame plan (tuning frame_plan, plan.hip): consecutive one-frame launches of a
