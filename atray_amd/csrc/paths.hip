@@ -208,7 +208,10 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
 // Leaf buffer entries of the bounce rays' queries (the scan is templated on it). 6 entries cut the
 // LDS to 18 KB per workgroup, enough for 8 waves/SIMD, but cost re-walks: c4 71.0 ms per frame at 7
 // waves and 72.1 at 8 (64 VGPRs, scratch in the hot loop) vs 69.5 with 8 entries.
-constexpr int kBounceLeafBuf = kLeafBuf;
+#ifndef ATR_BOUNCE_LEAFBUF
+#define ATR_BOUNCE_LEAFBUF kLeafBuf
+#endif
+constexpr int kBounceLeafBuf = ATR_BOUNCE_LEAFBUF;  // experiment builds: -DATR_BOUNCE_LEAFBUF=6
 template <bool COUNT, int OCC, bool SORT>
 __global__ __launch_bounds__(256, OCC) void path_bounce_kernel(PathParams P) {
     const int lane = threadIdx.x & 63;
@@ -438,7 +441,15 @@ __global__ __launch_bounds__(256) void path_sort_rank(PathParams P) {
 // camera kernel at 7 spills 21 dwords whose write-backs reach HBM (14.9 GB per c4 frame against
 // 4.6 GB at 6) and is no faster.
 constexpr int kCameraOcc = 6;
-constexpr int kBounceOcc = 7;
+#ifndef ATR_BOUNCE_OCC
+#define ATR_BOUNCE_OCC 7
+#endif
+constexpr int kBounceOcc = ATR_BOUNCE_OCC;
+#if ATR_BOUNCE_OCC == 8  // experiment: the bounce kernel at 8 waves/SIMD (needs a 6-leaf buffer's LDS)
+#define ATR_PATH_BOUNCE8(SORT) template __global__ void path_bounce_kernel<false, 8, SORT>(PathParams);
+#else
+#define ATR_PATH_BOUNCE8(SORT)
+#endif
 #define ATR_PATH_KERNELS(SORT)                                                  \
     template __global__ void path_camera_kernel<false, 5, SORT>(PathParams);    \
     template __global__ void path_camera_kernel<false, 6, SORT>(PathParams);    \
@@ -447,6 +458,7 @@ constexpr int kBounceOcc = 7;
     template __global__ void path_bounce_kernel<false, 5, SORT>(PathParams);    \
     template __global__ void path_bounce_kernel<false, 6, SORT>(PathParams);    \
     template __global__ void path_bounce_kernel<false, 7, SORT>(PathParams);    \
+    ATR_PATH_BOUNCE8(SORT)                                                      \
     template __global__ void path_bounce_kernel<true, 4, SORT>(PathParams);
 ATR_PATH_KERNELS(false)
 ATR_PATH_KERNELS(true)
@@ -470,6 +482,9 @@ void launch_bounce(const atr::PathParams& P, int occ, dim3 g, hipStream_t s) {
     if (P.counters) hipLaunchKernelGGL((atr::path_bounce_kernel<true, 4, SORT>), g, b, 0, s, P);
     else if (occ == 5) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 5, SORT>), g, b, 0, s, P);
     else if (occ == 6) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 6, SORT>), g, b, 0, s, P);
+#if ATR_BOUNCE_OCC == 8
+    else if (occ == 8) hipLaunchKernelGGL((atr::path_bounce_kernel<false, 8, SORT>), g, b, 0, s, P);
+#endif
     else hipLaunchKernelGGL((atr::path_bounce_kernel<false, 7, SORT>), g, b, 0, s, P);
 }
 }  // namespace
