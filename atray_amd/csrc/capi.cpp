@@ -672,10 +672,11 @@ hipError_t launch_paths_range(atr_ctx* c, const RenderParams& P, hipStream_t s, 
     return hipEventRecord(ws->ev, s);
 }
 
-// The path engine over a launch's cell list. A launch that is one batch (a single frame, c4's
-// 2 M-pixel frame at 64 spp) runs as two half batches on the context's two split streams, forked
-// from and joined back into s, so one half's level tails and queue sorts overlap the other half's
-// tracing (tuning path_split; outputs do not depend on the batching).
+// The path engine over a launch's cell list. With tuning path_split = 1 a launch that is one batch
+// (a single frame: c4's 2 M-pixel frame at 64 spp) runs as two half batches on the context's two
+// split streams, forked from and joined back into s, so one half's level tails and queue sorts
+// could overlap the other half's tracing; off by default (one c4 frame measured 61.1 vs 60.3 ms,
+// DESIGN.md §4h). Outputs do not depend on the batching.
 constexpr int64_t kSplitMinCells = 1024;
 hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
     if (P.nblocks <= 0) return hipSuccess;

@@ -232,6 +232,8 @@ constexpr int kSortDirs = ATR_SORT_DIRS;  // direction cells per side of the oct
 constexpr int kMaxSortBits = 7;
 constexpr int64_t kSortBinsMax = int64_t(1) << 26;  // 256 direction cells x 6 bits per axis
 constexpr int32_t kSortChunk = 4096;  // bins per block of the bin scan
+static_assert((kSortDirs * kSortDirs << 6) % kSortChunk == 0, "the fewest bins (2 bits per axis) fill whole scan blocks");
+static_assert((kSortBinsMax / kSortChunk) <= 32768, "path_sort_part_scan: one workgroup, 32 sums per lane");
 struct PathSort {
     int32_t bits;      // 0: off
     int32_t nbins;     // kSortDirs^2 << 3 bits

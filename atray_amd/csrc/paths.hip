@@ -489,7 +489,8 @@ void launch_bounce(const atr::PathParams& P, int occ, dim3 g, hipStream_t s) {
 }
 }  // namespace
 
-// With P.sort.bits > 0 the launch's survivors go to the staging queue (the queue sort, PathSort).
+// With P.sort.bits > 0 the launch reads and writes entry-major queues and its survivors record
+// their sort keys and ranks (the queue sort, PathSort).
 extern "C" hipError_t atr_launch_path_camera(const atr::PathParams& P, int occ, hipStream_t s) {
     const int64_t waves = int64_t(P.ncells) * P.cam.samples_per_pixel;
     if (waves <= 0) return hipSuccess;
