@@ -525,6 +525,9 @@ enum { SCHED_LANE = 0, SCHED_FLAT = 6, SCHED_HYBRID = 7 };
 // LDS leaf buffer), BOUNCE rays (incoherent: dealt rounds, register leaf buffer), PRIMARY-only
 // frames (CAMERA without u and v).
 enum { FLAV_CAMERA = 0, FLAV_BOUNCE = 1, FLAV_PRIMARY = 2, FLAV_HYB_BOUNCE = 3 };
+#ifndef ATR_BOUNCE_HYB  // experiment builds: 1 = the path engine's bounce rays choose lane-private or
+#define ATR_BOUNCE_HYB 0  // dealt leaf steps per step as HYBRID does (thresholds hybrid_a, hybrid_b)
+#endif
 
 // A model's table pointers as wave-uniform GLOBAL pointers (uniform_global, trace.h): read once per
 // query into SGPRs and cast to the global address space (through the DScene reference the compiler
@@ -578,7 +581,8 @@ __device__ __forceinline__ SceneHit intersect_models(const DScene* __restrict__ 
             else if constexpr (FLAV == FLAV_HYB_BOUNCE)
                 tree_closest_flat<COUNT, true, false, false, false, false>(r, m, active, h, err, ct, hyb_a, hyb_b);
             else  // bounce rays: near-first passes into the LDS leaf buffer, every step dealt
-                tree_closest_flat<COUNT, false, true, false, false, false, true, KB>(r, m, active, h, err, ct);
+                tree_closest_flat<COUNT, ATR_BOUNCE_HYB != 0, true, false, false, false, true, KB>(r, m, active, h, err, ct,
+                                                                                         hyb_a, hyb_b);
             if (h.t > kTol && h.t < sh.best) { sh.best = h.t; sh.face = h.face; sh.fu = h.u; sh.fv = h.v; sh.nm = i; }
         } else if (active) {  // brute force (:58-82), face-ordered triangles, uniform loads
             if constexpr (COUNT) { ct.box += 1; ct.box_all += 1; }
