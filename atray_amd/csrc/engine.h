@@ -218,8 +218,9 @@ struct PathCtl {
 };
 // Queue sort (tuning path_sort_bits = b > 0): the queues are entry-major (an entry's
 // four records together, q[4 e + i], 64 B) and every queued path also records {key, rank} in `kr`:
-// key = the ray's direction cell (kSortDirs^2 octahedral cells) above a Morton code of its origin
-// quantised to b bits per axis over the scene box (lo, sc = 2^b / extent), rank = its arrival
+// key = the ray's coarse direction cell (4 x 4 of the 16 x 16 octahedral cells), a Morton code of
+// its origin quantised to b bits per axis over the scene box (lo, sc = 2^b / extent), then its fine
+// direction cell within the coarse one (paths.hip path_sort_key), rank = its arrival
 // in the key's bin (atomicAdd on hist). The sort launches turn hist into bin starts and write the
 // level's key order perm[start[key] + rank] = entry; the next bounce launch's waves claim positions
 // of that order, so a wavefront takes rays of one direction cell and one region together (a

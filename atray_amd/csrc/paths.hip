@@ -22,6 +22,10 @@
 
 #include "scan.h"
 
+#ifndef ATR_SORT_ILEAVE  // fine direction bits per side below the origin cell (0: direction, then origin)
+#define ATR_SORT_ILEAVE 2
+#endif
+
 
 namespace atr {
 
@@ -50,8 +54,8 @@ __device__ __forceinline__ void path_finish(float4_t* out, uint32_t o, V3 ret, u
 }
 
 // Sort key of a queued ray (PathSort, engine.h): the octahedral cell of its direction (kSortDirs x
-// kSortDirs over the unfolded octahedron) above the Morton code of its origin's cell, b bits per axis
-// over the scene box.
+// kSortDirs over the unfolded octahedron) and the Morton code of its origin's cell, b bits per axis
+// over the scene box, interleaved as below.
 __device__ __forceinline__ uint32_t spread3(uint32_t x) {  // bits 0..9 -> every third bit
     x = (x | (x << 16)) & 0x030000FFu;
     x = (x | (x << 8)) & 0x0300F00Fu;
@@ -76,7 +80,13 @@ __device__ __forceinline__ uint32_t path_sort_key(V3 o, V3 d, PathSort so) {
     constexpr float D = float(kSortDirs);
     const uint32_t iu = uint32_t(fminf(fmaxf((u * 0.5f + 0.5f) * D, 0.0f), D - 1.0f));
     const uint32_t iv = uint32_t(fminf(fmaxf((v * 0.5f + 0.5f) * D, 0.0f), D - 1.0f));
-    return ((iv * uint32_t(kSortDirs) + iu) << (3 * so.bits)) | morton;
+    // coarse direction cell (the low F bits of iu, iv dropped), origin cell, then the fine bits:
+    // a run of the order is one coarse direction and one region, fine directions side by side
+    // (F = 2 of the 16 x 16 map: c4 +1.2%, c5 +1.5% over direction cell, then origin)
+    constexpr int F = ATR_SORT_ILEAVE;
+    const uint32_t coarse = (iv >> F) * uint32_t(kSortDirs >> F) + (iu >> F);
+    const uint32_t fine = ((iv & ((1u << F) - 1u)) << F) | (iu & ((1u << F) - 1u));
+    return (((coarse << (3 * so.bits)) | morton) << (2 * F)) | fine;
 }
 
 // Append this lane's path (if `go`) to queue q (planes `cap` entries apart): one atomic per wave for
