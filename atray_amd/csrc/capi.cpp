@@ -589,9 +589,11 @@ hipError_t launch_paths_range(atr_ctx* c, const RenderParams& P, hipStream_t s, 
             cells = std::min<int64_t>(batch, cend - cbeg);
             // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
             // one-frame launch already holds the batch of the multi-frame launches that follow it
-            int64_t cap = 1;
-            while (cap < cells * per_cell) cap <<= 1;
-            cap = std::max(cells * per_cell, std::min(cap, batch * per_cell));
+            // capacity: this launch's paths rounded up to 2^20 (at most a full batch): a one-frame c4
+            // launch holds its 132.7 M paths (20.7 GB), not a whole 2^28 batch; a later launch that
+            // needs more regrows the workspace once
+            const int64_t need = cells * per_cell, gran = int64_t(1) << 20;
+            const int64_t cap = std::max(need, std::min((need + gran - 1) / gran * gran, batch * per_cell));
             e = path_workspace(c, s, cap, std::max(levels, 8), bins, ws);
             if (e == hipSuccess && ws->cap < cap) e = hipErrorOutOfMemory;
         }
@@ -708,10 +710,15 @@ hipError_t launch_paths(atr_ctx* c, const RenderParams& P, hipStream_t s) {
 
 hipError_t launch_kernels(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
     if (sched == kSchedPaths) {
-        const hipError_t e = launch_paths(c, P, s);
+        hipError_t e = launch_paths(c, P, s);
         if (e != hipErrorOutOfMemory) return e;
-        sched = sched_of(ATR_KERNEL_FLAT);  // no memory for a path workspace: the cell megakernel,
-    }                                        // which needs none (same outputs)
+        // no memory for a path workspace: the cell megakernel, which needs none (same outputs,
+        // DESIGN.md §4). A split launch may have rendered its first half already: every output is
+        // rewritten, and the traced-ray counters (always a launch's zeroed ring set of 64 spread
+        // counters, launch_render) start again from zero so no ray is counted twice.
+        if (P.traced_rays && (e = hipMemsetAsync(P.traced_rays, 0, kTraceBytes, s)) != hipSuccess) return e;
+        sched = sched_of(ATR_KERNEL_FLAT);
+    }
     return atr_launch_render(P, sched, c->tune.primary_occ, s);
 }
 
@@ -1021,6 +1028,8 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
         (t->path_sort_bits != 0 && (t->path_sort_bits < 2 || t->path_sort_bits > kMaxSortBits)) ||
         t->path_split < 0 || t->path_split > 1)
         return ATR_E_INVALID;
+    for (int32_t r : t->reserved)  // room for later knobs: must be zero
+        if (r != 0) return ATR_E_INVALID;
     c->tune = *t;
     return ATR_OK;
 }
@@ -1110,8 +1119,20 @@ int atr_scene_upload(atr_ctx* c, const atr_material* mats, int32_t nmats, const 
             box[0] = std::min(box[0], v.x), box[1] = std::min(box[1], v.y), box[2] = std::min(box[2], v.z);
             box[3] = std::max(box[3], v.x), box[4] = std::max(box[4], v.y), box[5] = std::max(box[5], v.z);
         }
-    if (box[0] <= box[3] && box[1] <= box[4] && box[2] <= box[5])
-        std::memcpy(c->scene_box, box, sizeof(box));
+    for (int32_t i = 0; i < nspheres; ++i) {  // a sphere's bounds (planes are unbounded: left out)
+        const atr_sphere& sp = spheres[i];
+        const float r = std::fabs(sp.radius);
+        box[0] = std::min(box[0], sp.center.x - r), box[1] = std::min(box[1], sp.center.y - r);
+        box[2] = std::min(box[2], sp.center.z - r), box[3] = std::max(box[3], sp.center.x + r);
+        box[4] = std::max(box[4], sp.center.y + r), box[5] = std::max(box[5], sp.center.z + r);
+    }
+    // the queue sort's origin cells span this box; a scene with nothing bounded gets the unit box
+    // (not the previous upload's)
+    const float unit[6] = {0.f, 0.f, 0.f, 1.f, 1.f, 1.f};
+    const bool finite = std::isfinite(box[0]) && std::isfinite(box[1]) && std::isfinite(box[2]) &&
+                        std::isfinite(box[3]) && std::isfinite(box[4]) && std::isfinite(box[5]);
+    std::memcpy(c->scene_box, finite && box[0] <= box[3] && box[1] <= box[4] && box[2] <= box[5] ? box : unit,
+                sizeof(box));
     for (int32_t i = 0; i < nmodels; ++i) {
         const atr_model& md = models[i];
         const HostMesh& M = md.mesh->m;

@@ -94,7 +94,8 @@ class atr_tuning(C.Structure):
     _fields_ = [("xcd_chunk", C.c_int32), ("frame_rotate", C.c_int32), ("hybrid_a", C.c_int32),
                 ("hybrid_b", C.c_int32), ("path_batch_log2", C.c_int32), ("cluster_size", C.c_int32),
                 ("frame_plan", C.c_int32), ("path_camera_occ", C.c_int32), ("path_bounce_occ", C.c_int32),
-                ("primary_occ", C.c_int32), ("path_sort_bits", C.c_int32), ("path_split", C.c_int32)]
+                ("primary_occ", C.c_int32), ("path_sort_bits", C.c_int32), ("path_split", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 # every symbol include/atray.h declares (checked by tests/test_capi_symbols.py)

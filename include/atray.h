@@ -23,7 +23,9 @@
 extern "C" {
 #endif
 
-#define ATR_ABI_VERSION 1
+/* ABI 2 (round 6): atr_tuning gained reserved[4] (zero; room for later knobs without a size
+   change); ABI 1's last two words became path_sort_bits and path_split in round 5. */
+#define ATR_ABI_VERSION 2
 
 enum {
     ATR_OK = 0,
@@ -165,8 +167,10 @@ typedef struct {
                                cluster count exceeds a x rounds + b, -4096..4096; default 2, 0 */
     int32_t path_batch_log2; /* PATHS: paths per batch = 2^this (the path queues hold one batch,
                                144 B per path, 156 with the queue sort), 12..28; default 28
-                               (1920x1080 at 64 spp: a frame in one batch). 2^29 measured 5-7x
-                               slower */
+                               (1920x1080 at 64 spp: a frame in one batch). A workspace holds the
+                               launch's paths rounded up to 2^20, at most one batch: 20.7 GB for a
+                               1920x1080 64-spp frame, 42 GB at most (4 per context: 167 GB).
+                               2^29 measured 5-7x slower */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
     int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
                                dispatches its tiles' cells by that launch's measured cost, heaviest
@@ -187,6 +191,7 @@ typedef struct {
     int32_t path_split;     /* PATHS: 1 = a launch that is one batch (a single frame) runs as two
                                half batches on two internal streams, forked from and joined back
                                into the render's stream; 0 = one stream */
+    int32_t reserved[4];    /* must be 0 (ATR_E_INVALID otherwise) */
 } atr_tuning;
 void atr_default_tuning(atr_tuning* out);
 int atr_set_tuning(atr_ctx* ctx, const atr_tuning* tuning);

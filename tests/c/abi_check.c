@@ -39,7 +39,7 @@ static int layout(void) {
     SZ(atr_tuning); OFF(atr_tuning, xcd_chunk); OFF(atr_tuning, frame_rotate); OFF(atr_tuning, hybrid_a);
     OFF(atr_tuning, hybrid_b); OFF(atr_tuning, path_batch_log2); OFF(atr_tuning, cluster_size);
     OFF(atr_tuning, frame_plan); OFF(atr_tuning, path_camera_occ); OFF(atr_tuning, path_bounce_occ); OFF(atr_tuning, primary_occ);
-    OFF(atr_tuning, path_sort_bits); OFF(atr_tuning, path_split);
+    OFF(atr_tuning, path_sort_bits); OFF(atr_tuning, path_split); OFF(atr_tuning, reserved);
     printf("\"abi_version\": %d}\n", ATR_ABI_VERSION);
     return 0;
 }

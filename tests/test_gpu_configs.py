@@ -180,7 +180,7 @@ def test_c3_timed_shape_launch(eng, oracle_scene):
     cameras at 1920x1080, 1 spp, 1 bounce -> the 7-wave HYBRID primary kernel of multi-frame
     launches, graded cell order from calibration frames), with the app camera as one of the frames:
       * that frame reproduces the reference hash 43ad95dbe7a70300 with 284,360 hits (SURVEY 8(c));
-      * every other frame equals its one-camera render (the 6-wave single-frame kernel);
+      * every other frame equals its one-camera render (the 8-wave single-frame kernel);
       * one row band per frame matches the oracle (renderer.cpp:294-369, kd_tree.cpp:337-465).
     Round 4's only GPU fault (an illegal address in a reverted change) happened
     at this shape, which no test covered."""

@@ -2,6 +2,7 @@
 golden vectors. Bit-exact face index and t bits for primary hits; framebuffer and ray_casts
 bit-exact and RGB within 1e-5 relative (north star) for multi-bounce renders -- in practice the
 RGB is bit-exact too and the test reports it. Needs an MI355X (-m gpu)."""
+import ctypes as C
 import os
 
 import numpy as np
@@ -318,6 +319,10 @@ def test_tuning_changes_no_output(eng, variant):
             eng.set_tuning(path_sort_bits=bits)
     with pytest.raises(E.AtrError):
         eng.set_tuning(path_split=2)
+    t = E.atr_tuning()  # ABI 2: the reserved words must stay zero
+    assert E.lib().atr_get_tuning(eng.h, C.byref(t)) == 0
+    t.reserved[1] = 3
+    assert E.lib().atr_set_tuning(eng.h, C.byref(t)) == -1  # ATR_E_INVALID
     assert eng.tuning() == base
 
 

@@ -17,6 +17,9 @@ def test_fast_reciprocal_is_correctly_rounded():
         pytest.skip("no GPU")
     exe = os.path.join(ROOT, "atray_amd", "_lib", "recip_check")
     assert os.path.exists(exe), "build first: make -C atray_amd/csrc"
+    # never a stale binary: it must be newer than every source it is built from
+    for src in ("tests/c/recip_check.hip", "atray_amd/csrc/trace.h", "atray_amd/csrc/engine.h"):
+        assert os.path.getmtime(exe) >= os.path.getmtime(os.path.join(ROOT, src)), f"recip_check older than {src}"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "recip mismatches 0 checked 654311424" in r.stdout, r.stdout

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5 A/B, general form: variants "prod", "exp=<name>" (atray_amd/_lib/exp/<name>.so) or
+# A/B of the product library against experiments, general form: variants "prod", "exp=<name>" (atray_amd/_lib/exp/<name>.so) or
 # "tune=<k=v,...>" (product library, bench.py --tuning), "exp=<name>@<k=v,...>" (both) or
 # "args=<arg>+<arg>..." (product library, these bench.py arguments, e.g. args=--streams=1),
 # interleaved twice, on the configs given.
-# usage: gpu_r5_ab2.sh OUTDIR "variant ..." "c3 c4" [tests]
+# usage: gpu_ab.sh OUTDIR "variant ..." "c3 c4" [tests]
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/$1
