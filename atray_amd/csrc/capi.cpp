@@ -45,6 +45,11 @@ extern "C" hipError_t atr_launch_plan(const atr::DBlock* base, int32_t nb, unsig
                                       float split2, float split4, hipStream_t s);
 extern "C" size_t atr_plan_work_bytes(int32_t nb);
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s);
+extern "C" int64_t atr_masked_chunks(int64_t n);
+extern "C" hipError_t atr_launch_pack_bgr_masked(const uint32_t* src, int64_t n, uint32_t bg, uint8_t* out,
+                                                 int64_t* nbytes, hipStream_t s);
+extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n, const int64_t* dst_index,
+                                                    uint32_t* image, hipStream_t s);
 extern "C" hipError_t atr_launch_scatter_bgr(const uint8_t* src, int64_t n, const int64_t* dst_index,
                                              uint32_t* image, hipStream_t s);
 
@@ -1800,6 +1805,30 @@ int atr_scatter_bgr(atr_ctx* c, const uint8_t* packed, int64_t npixels, const in
     return ATR_OK;
 }
 
+int64_t atr_pack_bgr_masked_bound(int64_t npixels) {
+    if (npixels < 0) return ATR_E_INVALID;
+    const int64_t nc = atr_masked_chunks(npixels);
+    return 16 + 4 * nc + 1024 * nc + 3 * npixels;
+}
+
+int atr_pack_bgr_masked(atr_ctx* c, const uint32_t* framebuffer, int64_t npixels, uint32_t background, uint8_t* out,
+                        int64_t* nbytes, void* stream) {
+    if (!c || npixels < 0 || npixels >= (int64_t(1) << 32) || !out || !nbytes || (npixels && !framebuffer))
+        return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(atr_launch_pack_bgr_masked(framebuffer, npixels, background, out, nbytes, static_cast<hipStream_t>(stream)));
+    return ATR_OK;
+}
+
+int atr_scatter_bgr_masked(atr_ctx* c, const uint8_t* packed, int64_t npixels, const int64_t* dst_index,
+                           uint32_t* image, void* stream) {
+    if (!c || npixels < 0 || npixels >= (int64_t(1) << 32) || (npixels && (!packed || !dst_index || !image)))
+        return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(atr_launch_scatter_bgr_masked(packed, npixels, dst_index, image, static_cast<hipStream_t>(stream)));
+    return ATR_OK;
+}
+
 int atr_render_plan_info(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width, int32_t height,
                          int32_t* base_out, uint32_t* mask_hi_lo_out, int64_t cap, uint64_t* cost_out,
                          int64_t* nplanned) {
@@ -1902,6 +1931,13 @@ int atr_memcpy_d2h(atr_ctx* c, void* dst, const void* src, size_t bytes) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return ATR_OK;
+}
+int atr_memcpy_h2d(atr_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c || !dst || !src) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());  // a render may still read the destination
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
     return ATR_OK;
 }
 int atr_memset_d(atr_ctx* c, void* p, int v, size_t bytes) {

@@ -29,6 +29,146 @@ __global__ __launch_bounds__(256) void scatter_bgr_kernel(const uint8_t* __restr
     image[dst_index[i]] = v;
 }
 
+
+// ---------------------------------------------------------------- masked (background) exchange
+// Lossless, for frames that are mostly one value (c3: 86% of the pixels are the sky's colour): a
+// bit per pixel "not the background" plus 3 bytes for each such pixel only. Stream layout (bytes):
+//   [0, 16)        magic 'ATRM', bg (BGRX u32), nchunk, payload pixels in all
+//   [16, +4 n)     payload pixel offset of each 8192-pixel chunk (exclusive prefix)
+//   then           256 mask words (u32) per chunk, bit i of word k = pixel 32 k + i of the chunk
+//   then           3 bytes (B, G, R) per non-background pixel, in pixel order
+// Encoder: masks and per-chunk counts (one ballot per 64 pixels), the counts' scan (one
+// workgroup), the payload; decoder: one pass, each wave deriving its offset from the masks.
+constexpr int kMaskChunk = 8192;  // pixels per chunk = 4 waves x 32 groups of 64
+constexpr uint32_t kMaskMagic = 0x4D525441u;  // "ATRM"
+
+__device__ __forceinline__ uint32_t* mask_words(uint8_t* base, int64_t nchunk) {
+    return reinterpret_cast<uint32_t*>(base + 16 + 4 * nchunk);
+}
+
+// Wave w of chunk c covers pixels c * 8192 + w * 2048 + [0, 2048): 32 groups of 64.
+__global__ __launch_bounds__(256) void masked_count_kernel(const uint32_t* __restrict__ src, int64_t n, uint32_t bg,
+                                                           uint8_t* __restrict__ out, int64_t nchunk) {
+    __shared__ uint32_t part[4];
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int64_t c = blockIdx.x;
+    uint32_t* mw = mask_words(out, nchunk) + c * (kMaskChunk / 32) + w * 64;
+    const int64_t p0 = c * kMaskChunk + int64_t(w) * 2048;
+    uint32_t cnt = 0;
+    for (int g = 0; g < 32; ++g) {
+        const int64_t i = p0 + g * 64 + ln;
+        const bool nb = i < n && src[i] != bg;
+        const unsigned long long m = __ballot(nb);
+        if (ln == 0) {
+            mw[2 * g] = uint32_t(m);
+            mw[2 * g + 1] = uint32_t(m >> 32);
+        }
+        cnt += uint32_t(__popcll(m));
+    }
+    if (ln == 0) part[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        reinterpret_cast<uint32_t*>(out + 16)[c] = part[0] + part[1] + part[2] + part[3];
+}
+
+// Exclusive scan of the chunk counts in place (one workgroup, 1024 chunks per pass), the header
+// and the stream's byte count.
+__global__ __launch_bounds__(1024) void masked_scan_kernel(uint8_t* __restrict__ out, int64_t nchunk, uint32_t bg,
+                                                           int64_t* __restrict__ nbytes) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry_s;
+    uint32_t* off = reinterpret_cast<uint32_t*>(out + 16);
+    const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    for (int64_t b = 0; b < nchunk; b += 1024) {
+        const int64_t i = b + threadIdx.x;
+        const uint32_t v = i < nchunk ? off[i] : 0u;
+        uint32_t x = v;  // inclusive scan within the wave
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = uint32_t(__shfl_up(int(x), d));
+            if (ln >= d) x += y;
+        }
+        if (ln == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = carry_s;
+        for (int k = 0; k < w; ++k) before += wsum[k];
+        if (i < nchunk) off[i] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry_s = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint32_t* h = reinterpret_cast<uint32_t*>(out);
+        h[0] = kMaskMagic;
+        h[1] = bg;
+        h[2] = uint32_t(nchunk);
+        h[3] = carry_s;
+        *nbytes = 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk + 3 * int64_t(carry_s);
+    }
+}
+
+// A wave's first payload pixel: its chunk's offset plus the popcounts of the earlier waves' masks.
+__device__ __forceinline__ uint32_t masked_wave_base(const uint32_t* off, const uint32_t* mw_chunk, int w, int ln) {
+    __shared__ uint32_t part[4];
+    uint32_t cnt = uint32_t(__popc(mw_chunk[w * 64 + ln]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += uint32_t(__shfl_xor(int(cnt), o));
+    if (ln == 0) part[w] = cnt;
+    __syncthreads();
+    uint32_t b = off[blockIdx.x];
+    for (int k = 0; k < w; ++k) b += part[k];
+    return b;
+}
+
+__global__ __launch_bounds__(256) void masked_payload_kernel(const uint32_t* __restrict__ src, int64_t n,
+                                                             uint8_t* __restrict__ out, int64_t nchunk) {
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int64_t c = blockIdx.x;
+    const uint32_t* mw = mask_words(out, nchunk) + c * (kMaskChunk / 32);
+    uint32_t base = masked_wave_base(reinterpret_cast<const uint32_t*>(out + 16), mw, w, ln);
+    uint8_t* pay = reinterpret_cast<uint8_t*>(mask_words(out, nchunk) + nchunk * (kMaskChunk / 32));
+    const int64_t p0 = c * kMaskChunk + int64_t(w) * 2048;
+    const unsigned long long below = (ln ? ~0ull >> (64 - ln) : 0ull);
+    for (int g = 0; g < 32; ++g) {
+        const unsigned long long m = uint64_t(mw[w * 64 + 2 * g]) | (uint64_t(mw[w * 64 + 2 * g + 1]) << 32);
+        if ((m >> ln) & 1) {
+            const uint32_t v = src[p0 + g * 64 + ln];
+            uint8_t* d = pay + 3 * int64_t(base + uint32_t(__popcll(m & below)));
+            d[0] = uint8_t(v);
+            d[1] = uint8_t(v >> 8);
+            d[2] = uint8_t(v >> 16);
+        }
+        base += uint32_t(__popcll(m));
+    }
+}
+
+__global__ __launch_bounds__(256) void masked_scatter_kernel(const uint8_t* __restrict__ in, int64_t n,
+                                                             const int64_t* __restrict__ dst_index,
+                                                             uint32_t* __restrict__ image, int64_t nchunk) {
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int64_t c = blockIdx.x;
+    const uint32_t bg = reinterpret_cast<const uint32_t*>(in)[1];
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk) + c * (kMaskChunk / 32);
+    uint32_t base = masked_wave_base(reinterpret_cast<const uint32_t*>(in + 16), mw, w, ln);
+    const uint8_t* pay = in + 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk;
+    const int64_t p0 = c * kMaskChunk + int64_t(w) * 2048;
+    const unsigned long long below = (ln ? ~0ull >> (64 - ln) : 0ull);
+    for (int g = 0; g < 32; ++g) {
+        const unsigned long long m = uint64_t(mw[w * 64 + 2 * g]) | (uint64_t(mw[w * 64 + 2 * g + 1]) << 32);
+        const int64_t i = p0 + g * 64 + ln;
+        if (i < n) {
+            uint32_t v = bg;
+            if ((m >> ln) & 1) {
+                const uint8_t* s = pay + 3 * int64_t(base + uint32_t(__popcll(m & below)));
+                v = uint32_t(s[0]) | (uint32_t(s[1]) << 8) | (uint32_t(s[2]) << 16);
+            }
+            image[dst_index[i]] = v;
+        }
+        base += uint32_t(__popcll(m));
+    }
+}
+
 }  // namespace atr
 
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s) {
@@ -42,5 +182,30 @@ extern "C" hipError_t atr_launch_scatter_bgr(const uint8_t* src, int64_t n, cons
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(atr::scatter_bgr_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, src, n,
                        dst_index, image);
+    return hipGetLastError();
+}
+
+extern "C" int64_t atr_masked_chunks(int64_t n) { return (n + atr::kMaskChunk - 1) / atr::kMaskChunk; }
+
+extern "C" hipError_t atr_launch_pack_bgr_masked(const uint32_t* src, int64_t n, uint32_t bg, uint8_t* out,
+                                                 int64_t* nbytes, hipStream_t s) {
+    const int64_t nc = atr_masked_chunks(n);
+    if (nc > 0) {
+        hipLaunchKernelGGL(atr::masked_count_kernel, dim3(unsigned(nc)), dim3(256), 0, s, src, n, bg, out, nc);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(atr::masked_scan_kernel, dim3(1), dim3(1024), 0, s, out, nc, bg, nbytes);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nc == 0) return e;
+    hipLaunchKernelGGL(atr::masked_payload_kernel, dim3(unsigned(nc)), dim3(256), 0, s, src, n, out, nc);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n, const int64_t* dst_index,
+                                                    uint32_t* image, hipStream_t s) {
+    const int64_t nc = atr_masked_chunks(n);
+    if (nc <= 0) return hipSuccess;
+    hipLaunchKernelGGL(atr::masked_scatter_kernel, dim3(unsigned(nc)), dim3(256), 0, s, in, n, dst_index, image, nc);
     return hipGetLastError();
 }

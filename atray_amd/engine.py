@@ -107,11 +107,12 @@ EXPORTS = [
     "atr_scene_upload", "atr_scene_info", "atr_render_start", "atr_render_start_ex",
     "atr_render_counters", "atr_render_tile_costs", "atr_balance_shard_tiles",
     "atr_render_packed_size", "atr_packed_pixel_map", "atr_unpack", "atr_tile_ray_casts", "atr_render_wait",
-    "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h",
+    "atr_last_kernel_ms", "atr_device_alloc", "atr_device_free", "atr_memcpy_d2h", "atr_memcpy_h2d",
     "atr_memset_d", "atr_render_start_progressive", "atr_write_bmp", "atr_render_start_frames",
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_default_tuning", "atr_set_tuning", "atr_get_tuning", "atr_pack_bgr", "atr_scatter_bgr",
+    "atr_pack_bgr_masked_bound", "atr_pack_bgr_masked", "atr_scatter_bgr_masked",
     "atr_render_plan_info", "atr_workspace_info",
 ]
 # the diagnostic build's extra symbols (include/atray_diag.h; make -C atray_amd/csrc DIAG=1)
@@ -177,6 +178,9 @@ def lib():
         "atr_pack_bgr": ([vp, vp, i64, vp, vp], C.c_int),
         "atr_render_plan_info": ([vp, vp, i32, i32, i32, vp, vp, i64, vp, P(i64)], C.c_int),
         "atr_scatter_bgr": ([vp, vp, i64, vp, vp, vp], C.c_int),
+        "atr_pack_bgr_masked_bound": ([i64], i64),
+        "atr_pack_bgr_masked": ([vp, vp, i64, u32, vp, vp, vp], C.c_int),
+        "atr_scatter_bgr_masked": ([vp, vp, i64, vp, vp, vp], C.c_int),
         "atr_render_simd_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
@@ -191,6 +195,7 @@ def lib():
         "atr_device_alloc": ([vp, C.c_size_t, P(vp)], C.c_int),
         "atr_device_free": ([vp, vp], C.c_int),
         "atr_memcpy_d2h": ([vp, vp, vp, C.c_size_t], C.c_int),
+        "atr_memcpy_h2d": ([vp, vp, vp, C.c_size_t], C.c_int),
         "atr_memset_d": ([vp, vp, C.c_int, C.c_size_t], C.c_int),
     }
     for name in [n for n in DIAG_EXPORTS if not hasattr(L, n)]:
@@ -565,6 +570,19 @@ class Engine:
         check(lib().atr_scatter_bgr(self.h, C.c_void_p(packed_ptr), int(npixels), C.c_void_p(index_ptr),
                                     C.c_void_p(image_ptr), C.c_void_p(stream) if stream else None), "scatter bgr")
 
+    def pack_bgr_masked(self, fb_ptr, npixels, background, out_ptr, nbytes_ptr, stream=None):
+        """BGRX u32 -> the masked stream (atr_pack_bgr_masked: a bit per pixel, 3 bytes per pixel that
+        differs from `background`); its byte count goes to the device int64 at nbytes_ptr."""
+        check(lib().atr_pack_bgr_masked(self.h, C.c_void_p(fb_ptr), int(npixels), int(background) & 0xFFFFFFFF,
+                                        C.c_void_p(out_ptr), C.c_void_p(nbytes_ptr),
+                                        C.c_void_p(stream) if stream else None), "pack bgr masked")
+
+    def scatter_bgr_masked(self, packed_ptr, npixels, index_ptr, image_ptr, stream=None):
+        """A masked stream of npixels -> BGRX u32 at image[index[i]] (atr_scatter_bgr_masked)."""
+        check(lib().atr_scatter_bgr_masked(self.h, C.c_void_p(packed_ptr), int(npixels), C.c_void_p(index_ptr),
+                                           C.c_void_p(image_ptr), C.c_void_p(stream) if stream else None),
+              "scatter bgr masked")
+
     def plan_info(self, tiles, width, height):
         """The single-frame plan of a tile list (diagnostic): (base index per planned block, masks
         (n, 2) u32, cost per base block) or None before the first planned launch."""
@@ -634,6 +652,11 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+
+def pack_bgr_masked_bound(npixels):
+    """Largest masked exchange stream of npixels pixels, in bytes (atr_pack_bgr_masked_bound)."""
+    return int(lib().atr_pack_bgr_masked_bound(int(npixels)))
 
 
 def packed_size(tiles):

@@ -195,6 +195,32 @@ def gather_frames(send, recv, plan: ShardPlan, rank: int, nframes: int, dist, un
     return dist.batch_isend_irecv(ops) if ops else []
 
 
+def gather_sizes(nbytes, sizes, plan: ShardPlan, rank: int, dist):
+    """Phase 1 of the masked exchange: every rank's stream length (a (1,) int64 tensor) into rank 0's
+    `sizes` (world,) at index r. Ranks without pixels send nothing. Returns the async works."""
+    ops = []
+    if rank == 0:
+        for r in range(1, plan.world):
+            if plan.sizes[r]:
+                ops.append(dist.P2POp(dist.irecv, sizes[r:r + 1], r))
+    elif plan.sizes[rank]:
+        ops.append(dist.P2POp(dist.isend, nbytes, 0))
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
+def gather_streams(send, recv, roff, sizes, plan: ShardPlan, rank: int, dist):
+    """Phase 2 of the masked exchange: the exact streams to rank 0 (rank r's into recv[roff[r]:],
+    sizes[r] bytes, u8 tensors). `send` (other ranks): this rank's stream, exactly its length."""
+    ops = []
+    if rank == 0:
+        for r in range(1, plan.world):
+            if plan.sizes[r] and sizes[r]:
+                ops.append(dist.P2POp(dist.irecv, recv[int(roff[r]):int(roff[r]) + int(sizes[r])], r))
+    elif plan.sizes[rank] and send.numel():
+        ops.append(dist.P2POp(dist.isend, send, 0))
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
 def pack_bgr_host(fb) -> np.ndarray:
     """Host reference of atr_pack_bgr: BGRX u32 pixels -> 3 bytes each (B, G, R); the X byte must
     be 0 (texture.h:27-38), so nothing is lost."""
@@ -207,6 +233,50 @@ def scatter_bgr_host(packed, dst_index, image) -> None:
     """Host reference of atr_scatter_bgr: image[dst_index[i]] = B | G << 8 | R << 16."""
     p = np.asarray(packed, np.uint8).reshape(-1, 3).astype(np.uint32)
     image[np.asarray(dst_index, np.int64)] = p[:, 0] | (p[:, 1] << 8) | (p[:, 2] << 16)
+
+
+MASK_CHUNK = 8192  # pixels per chunk of the masked stream (exchange.hip)
+
+
+def background_value(fb) -> int:
+    """The most common BGRX value of a frame (the masked exchange's background: a c3 frame's sky).
+    Any value gives a correct stream; the common one gives the shortest."""
+    v, c = np.unique(np.asarray(fb, np.uint32), return_counts=True)
+    return int(v[np.argmax(c)]) if v.size else 0
+
+
+def pack_bgr_masked_host(fb, background: int) -> np.ndarray:
+    """Host reference of atr_pack_bgr_masked: the same bytes as the device stream (header, chunk
+    offsets, mask words, B, G, R of every pixel != background)."""
+    fb = np.ascontiguousarray(np.asarray(fb, np.uint32))
+    n = fb.size
+    nc = -(-n // MASK_CHUNK)
+    nb = np.zeros(nc * MASK_CHUNK, bool)
+    nb[:n] = fb != np.uint32(background)
+    words = np.packbits(nb.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel().astype("<u4")
+    counts = nb.reshape(nc, MASK_CHUNK).sum(1) if nc else np.zeros(0, np.int64)
+    off = (np.cumsum(counts) - counts).astype("<u4")
+    total = int(counts.sum())
+    hdr = np.array([0x4D525441, int(background) & 0xFFFFFFFF, nc, total], "<u4")
+    pay = pack_bgr_host(fb[nb[:n]]) if total else np.zeros(0, np.uint8)
+    return np.concatenate([hdr.view(np.uint8), off.view(np.uint8), words.view(np.uint8), pay])
+
+
+def scatter_bgr_masked_host(stream, npixels: int, dst_index, image) -> None:
+    """Host reference of atr_scatter_bgr_masked: image[dst_index[i]] = pixel i of the stream."""
+    b = np.asarray(stream, np.uint8)
+    hdr = b[:16].view("<u4")
+    assert int(hdr[0]) == 0x4D525441, "not a masked exchange stream"
+    bg, nc, total = int(hdr[1]), int(hdr[2]), int(hdr[3])
+    assert nc == -(-npixels // MASK_CHUNK)
+    w0 = 16 + 4 * nc
+    words = b[w0:w0 + 4 * nc * (MASK_CHUNK // 32)].view("<u4")
+    bits = np.unpackbits(words.astype(">u4").view(np.uint8).reshape(-1, 4), axis=1)
+    nb = bits.reshape(-1, 32)[:, ::-1].ravel()[:npixels].astype(bool)
+    vals = np.full(npixels, bg, np.uint32)
+    p = b[w0 + 4 * nc * (MASK_CHUNK // 32):][:3 * total].reshape(-1, 3).astype(np.uint32)
+    vals[nb] = p[:, 0] | (p[:, 1] << 8) | (p[:, 2] << 16)
+    image[np.asarray(dst_index, np.int64)] = vals
 
 
 def scatter_host(bufs, plan: ShardPlan) -> np.ndarray:

@@ -344,10 +344,12 @@ def main():
     ap.add_argument("--rank0-extra", type=float, default=-1.0,
                     help="rank 0's frame-assembly share, as a fraction of the mean per-rank load; "
                          "-1 (default): estimated from the calibration renders (S.assembly_share)")
-    ap.add_argument("--exchange", default="bgr", choices=["bgr", "bgrx"],
-                    help="N>1 frame exchange: 3 bytes per pixel (the framebuffer's X byte is always 0; "
-                         "atr_pack_bgr / atr_scatter_bgr; gloo rehearsals stage the bytes through the host) or the "
-                         "u32 BGRX framebuffer")
+    ap.add_argument("--exchange", default="masked", choices=["masked", "bgr", "bgrx"],
+                    help="N>1 frame exchange: masked (default, round 6): a bit per pixel plus 3 bytes for each "
+                         "pixel that differs from the background value (atr_pack_bgr_masked / "
+                         "atr_scatter_bgr_masked; c3 ~0.54 B/px; sizes first, then the exact streams); bgr: 3 bytes "
+                         "per pixel (the framebuffer's X byte is always 0; atr_pack_bgr / atr_scatter_bgr); bgrx: "
+                         "the u32 framebuffer. gloo rehearsals stage the bytes through the host")
     ap.add_argument("--check", action="store_true",
                     help="rank 0: compare every assembled frame with a one-launch full-frame render")
     ap.add_argument("--sim-world", type=int, default=0,
@@ -415,6 +417,41 @@ def selftest(args):
             casts[f] = pix % 5
         tsum = torch.zeros(F, ngrid, dtype=torch.int64).index_add_(1, stile, casts)
         bgr = args.exchange == "bgr"
+        if args.exchange == "masked":  # the masked exchange through its host references
+            bgv = 7 * k  # frame k's most common value (pixel index 0 + 7 k): any value is exact
+            st = S.pack_bgr_masked_host(fb[:nf * own].numpy().astype(np.uint32), bgv) if own else np.zeros(0, np.uint8)
+            nb = torch.tensor([st.size], dtype=torch.int64)
+            img = torch.zeros(F * W * H, dtype=torch.int64)
+            if world > 1:
+                sizes = torch.zeros(world, dtype=torch.int64)
+                for w_ in S.gather_sizes(nb, sizes if rank == 0 else None, plan, rank, dist):
+                    w_.wait()
+                bounds = [int(S.E.pack_bgr_masked_bound(nf * plan.sizes[r])) if plan.sizes[r] else 0
+                          for r in range(world)] if rank == 0 else None
+                roff = [0] + list(np.cumsum(bounds)) if rank == 0 else None
+                recv = torch.zeros(max(1, int(roff[-1])), dtype=torch.uint8) if rank == 0 else None
+                for w_ in S.gather_streams(torch.from_numpy(st), recv, roff, sizes.tolist() if rank == 0 else None,
+                                           plan, rank, dist):
+                    w_.wait()
+                for w_ in [dist.reduce(tsum, dst=0, async_op=True)]:
+                    w_.wait()
+            if rank == 0:
+                im = np.zeros(F * W * H, np.uint32)
+                if own:
+                    im[dst[off[0]:off[0] + nf * own].numpy()] = fb[:nf * own].numpy().astype(np.uint32)
+                for r in range(1, world):
+                    if plan.sizes[r]:
+                        S.scatter_bgr_masked_host(recv[int(roff[r]):].numpy(), nf * plan.sizes[r],
+                                                  dst[off[r]:off[r] + nf * plan.sizes[r]].numpy(), im)
+                img = torch.from_numpy(im.astype(np.int64))
+                want = torch.arange(W * H, dtype=torch.int64)
+                for f in range(nf):
+                    got = img[f * W * H:(f + 1) * W * H]
+                    mism += int((got != want + 7 * (k + f)).sum())
+                    casts_ok &= bool(torch.equal(tsum[f], want_tiles))
+                    frames += 1
+            k += nf
+            continue
         if bgr:  # the 3-byte exchange through the host references of atr_pack_bgr / atr_scatter_bgr
             big3 = torch.zeros(3 * F * W * H, dtype=torch.uint8)
             mine = torch.from_numpy(S.pack_bgr_host(fb[:F * own].numpy().astype(np.uint32)))
@@ -587,6 +624,7 @@ def run(args):
     # 3-byte exchange (atr_pack_bgr / atr_scatter_bgr on the device; a gloo rehearsal stages the
     # packed bytes through the host)
     bgr = pw > 1 and args.exchange == "bgr"
+    masked = pw > 1 and args.exchange == "masked"
     traced = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
     # per stream slot: F framebuffers and F ray_casts images (u32), frames back to back
     casts = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
@@ -602,7 +640,25 @@ def run(args):
         tids = torch.from_numpy(S.tile_ids(plan, pr)).to(dev)
         tcasts = [torch.zeros(F_, max(1, len(tids)), dtype=torch.int64, device=dev) for _ in range(S_)]
         tsum = [torch.zeros(F_, ngrid, dtype=torch.int64, device="cpu" if on_host else dev) for _ in range(S_)]
-        if bgr:
+        if masked:
+            # masked exchange: every rank encodes its F frames into one stream (atr_pack_bgr_masked);
+            # the streams' sizes go to rank 0 first, then the exact streams; rank 0 decodes each into
+            # the images through the assembly index and copies its own frames in directly
+            fbs = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
+            enc = [torch.zeros(E.pack_bgr_masked_bound(F_ * max(1, own)), dtype=torch.uint8, device=dev)
+                   for _ in range(S_)]
+            nbytes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(S_)]
+            if rank == 0 and not sim:
+                bounds = [E.pack_bgr_masked_bound(F_ * sizes[r]) if sizes[r] else 0 for r in range(world)]
+                roff = [0] + list(np.cumsum(bounds))
+                recv = [torch.zeros(max(1, int(roff[-1])), dtype=torch.uint8, device="cpu" if on_host else dev)
+                        for _ in range(S_)]
+                recv_dev = [torch.zeros(max(1, int(roff[-1])), dtype=torch.uint8, device=dev) for _ in range(S_)] \
+                    if on_host else recv
+                nsz = [torch.zeros(world, dtype=torch.int64, device="cpu" if on_host else dev) for _ in range(S_)]
+                dst_idx = torch.from_numpy(S.frames_assembly_index(plan, F_)).to(dev)
+                images = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
+        elif bgr:
             # 3-byte exchange: every rank packs its F frames into bytes (rank 0 straight into its
             # block of the byte gather buffer), rank 0 scatters the gathered bytes into the images
             fbs = [torch.zeros(F_ * max(1, own), dtype=torch.int32, device=dev) for _ in range(S_)]
@@ -630,7 +686,9 @@ def run(args):
         return E.atr_frame(layout, fbs[q].data_ptr(), None, None, None, casts[q].data_ptr(), traced[q].data_ptr())
 
     pending = {}
+    launch_nf = {}
     timing = [False]
+    bgv = [0]  # the masked exchange's background value (this rank's most common pixel, set below)
 
     def image_views(q, f):
         """(framebuffer, ray_casts or None) of frame f of stream slot q: (H*W,) views; at N > 1
@@ -650,6 +708,28 @@ def run(args):
         with torch.cuda.stream(streams[q]):
             for w_ in works:
                 w_.wait()
+            if masked:  # the sizes are in: the exact streams, then rank 0 decodes them
+                nf = launch_nf[j]
+                if rank == 0:
+                    sz = nsz[q].cpu().tolist()
+                    works2 = S.gather_streams(None, recv[q], roff, sz, plan, rank, dist)
+                else:
+                    mine = int(nbytes[q].item()) if own else 0
+                    src = enc[q][:mine].cpu() if on_host else enc[q][:mine]
+                    works2 = S.gather_streams(src, None, None, None, plan, rank, dist)
+                for w_ in works2:
+                    w_.wait()
+                if rank == 0:
+                    if on_host:
+                        recv_dev[q].copy_(recv[q])
+                    for r in range(1, world):
+                        if sizes[r]:
+                            eng.scatter_bgr_masked(recv_dev[q][int(roff[r]):].data_ptr(), nf * sizes[r],
+                                                   dst_idx[off[r]:].data_ptr(), images[q].data_ptr(),
+                                                   stream=streams[q].cuda_stream)
+                    if own:
+                        images[q].index_copy_(0, dst_idx[off[0]:off[0] + nf * own], fbs[q][:nf * own])
+                return
             if rank == 0 and bgr:
                 if on_host:
                     big[q].copy_(bigh[q])
@@ -688,8 +768,21 @@ def run(args):
                         ts.index_copy_(1, tids, part)
                 if bgr and own:  # the rank's frames in 3 bytes per pixel (part of its per-rank work)
                     eng.pack_bgr(fbs[q].data_ptr(), nf * own, send3[q].data_ptr(), stream=streams[q].cuda_stream)
+                if masked and own and pr != 0:  # the rank's frames as one masked stream (rank 0 keeps its own)
+                    eng.pack_bgr_masked(fbs[q].data_ptr(), nf * own, bgv[0], enc[q].data_ptr(), nbytes[q].data_ptr(),
+                                        stream=streams[q].cuda_stream)
+                launch_nf[j] = nf
                 if sim:
                     pending[j] = (q, [])
+                    return
+                if masked:  # phase 1: every stream's byte count to rank 0 (phase 2 in assemble)
+                    if on_host:
+                        torch.cuda.synchronize()
+                        works = S.gather_sizes(nbytes[q].cpu(), nsz[q] if rank == 0 else None, plan, rank, dist)
+                    else:
+                        works = S.gather_sizes(nbytes[q], nsz[q] if rank == 0 else None, plan, rank, dist)
+                    works.append(dist.reduce(ts, dst=0, async_op=True))
+                    pending[j] = (q, works)
                     return
                 if bgr:
                     if on_host:
@@ -733,6 +826,8 @@ def run(args):
         eng.render_start_cameras([cams[0]], tiles, frame_of(q), own, SEED, stream=streams[q].cuda_stream,
                                  variant=variant)
     torch.cuda.synchronize()
+    if masked and own:  # untimed: the background value from this rank's first frame (any value is exact)
+        bgv[0] = S.background_value(fbs[0][:own].cpu().numpy().view(np.uint32))
     if world > 1:
         dist.barrier()
     run_frames(0, args.warmup)
@@ -878,7 +973,8 @@ def run(args):
                           "plan": (f"{args.plan}/{args.tile_order}" if pw > 1 else
                                    "single" if args.single_tiles == "frame" else f"single/{args.tile_order}"),
                           "streams": args.streams, "frames_per_launch": F_,
-                          **({"exchange": "bgr (3 B/px)" if bgr else "bgrx (4 B/px)"} if pw > 1 else {}),
+                          **({"exchange": "masked (mask bit + 3 B per non-background px)" if masked else
+                              "bgr (3 B/px)" if bgr else "bgrx (4 B/px)"} if pw > 1 else {}),
                           "launches": launch_sizes(args.steps, F_, S_),
                           **({"rank0_extra": round(args.rank0_extra, 4)} if pw > 1 else {}),
                           "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),

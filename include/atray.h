@@ -319,6 +319,21 @@ int atr_packed_tile_ray_casts(atr_ctx* ctx, const atr_tile* tiles, int32_t ntile
 int atr_pack_bgr(atr_ctx* ctx, const uint32_t* framebuffer, int64_t npixels, uint8_t* out, void* stream);
 int atr_scatter_bgr(atr_ctx* ctx, const uint8_t* packed, int64_t npixels, const int64_t* dst_index, uint32_t* image,
                     void* stream);
+/* Lossless masked exchange (round 6): frames that are mostly one background value (a c3 frame is
+   86% sky) travel as a bit per pixel plus 3 bytes for each pixel that differs from `background`
+   (any value is correct; the common one compresses best): ~0.54 B per c3 pixel instead of 3.
+   Stream: a 16-byte header {magic "ATRM", background, chunks, payload pixels}, one u32 payload
+   offset per 8192-pixel chunk, 1 KB of mask bits per chunk, then B, G, R of every non-background
+   pixel in order. atr_pack_bgr_masked_bound(n) = the largest stream for n pixels (host, no device;
+   size `out` by it); atr_pack_bgr_masked writes the stream and its exact byte count to the DEVICE
+   int64 *nbytes (the sender ships that many bytes); atr_scatter_bgr_masked decodes a stream of
+   npixels into image[dst_index[i]] (as atr_scatter_bgr). Device pointers; async on `stream`;
+   npixels < 2^32. */
+int64_t atr_pack_bgr_masked_bound(int64_t npixels);
+int atr_pack_bgr_masked(atr_ctx* ctx, const uint32_t* framebuffer, int64_t npixels, uint32_t background, uint8_t* out,
+                        int64_t* nbytes, void* stream);
+int atr_scatter_bgr_masked(atr_ctx* ctx, const uint8_t* packed, int64_t npixels, const int64_t* dst_index,
+                           uint32_t* image, void* stream);
 /* Per-cell launch plan for renders of width x height (NULL clears): one byte per 8x8 cell (row
    major, ceil(W/8) x ceil(H/8)). Low nibble: the number of waves the cell is split into (0/1 =
    one, 2, 4 or 8 row bands: a heavy cell's rays then share their dealt leaf scans with 2-8x as
@@ -353,6 +368,7 @@ int atr_last_kernel_ms(atr_ctx* ctx, float* ms);
 int atr_device_alloc(atr_ctx* ctx, size_t bytes, void** dptr);
 int atr_device_free(atr_ctx* ctx, void* dptr);
 int atr_memcpy_d2h(atr_ctx* ctx, void* dst, const void* src, size_t bytes);
+int atr_memcpy_h2d(atr_ctx* ctx, void* dptr, const void* src, size_t bytes);
 int atr_memset_d(atr_ctx* ctx, void* dptr, int value, size_t bytes);
 
 #ifdef __cplusplus

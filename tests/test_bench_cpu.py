@@ -20,7 +20,7 @@ def _json_line(out):
     return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("n,exchange", [(2, "bgr"), (2, "bgrx"), (3, "bgr"), (8, "bgr")])
+@pytest.mark.parametrize("n,exchange", [(2, "bgr"), (2, "bgrx"), (3, "bgr"), (8, "bgr"), (2, "masked"), (3, "masked"), (8, "masked")])
 def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n, exchange):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):

@@ -2,7 +2,8 @@
 the graded cell order (atr_set_cell_plan classes), the packed shard renders, the frame exchange --
 3 bytes per pixel (atr_pack_bgr on each rank, atr_scatter_bgr on rank 0: the code the 8-GPU RCCL run
 uses, with the bytes staged through the host) or the u32 framebuffer --, frame assembly and the
-per-tile ray_casts reduction, on c3 (HYBRID) and c4 (the path engine). --check renders every timed frame again as one full-frame launch and
+per-tile ray_casts reduction, on c3 (HYBRID) and c4 (the path engine). Round 6: the masked exchange
+(the default: atr_pack_bgr_masked streams, their sizes sent first, atr_scatter_bgr_masked on rank 0). --check renders every timed frame again as one full-frame launch and
 counts mismatching pixels and tile sums: it must be 0 (the reordered block list once broke the
 per-tile counters). Two ranks, one subprocess tree (bench.py starts its ranks itself).
 Needs an MI355X (-m gpu)."""
@@ -17,8 +18,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("config,order,exchange", [("c3", "graded", "bgr"), ("c3", "list", "bgr"),
-                                                   ("c3", "graded", "bgrx"), ("c4", "graded", "bgr")])
+@pytest.mark.parametrize("config,order,exchange", [("c3", "graded", "masked"), ("c3", "list", "bgr"),
+                                                   ("c3", "graded", "bgrx"), ("c4", "graded", "masked"),
+                                                   ("c3", "graded", "bgr")])
 def test_bench_two_ranks_frames_exact(config, order, exchange):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():

@@ -608,6 +608,48 @@ def test_bgr_exchange_reassembles_frames(eng):
         assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
 
 
+@pytest.mark.parametrize("bgsel", ["sky", "first", "absent"])
+def test_masked_exchange_reassembles_frames(eng, bgsel):
+    """The masked exchange (atr_pack_bgr_masked / atr_scatter_bgr_masked, round 6): 3 ranks' packed
+    shard frames (2 per launch) encoded against a background value -- the frame's common sky value,
+    rank 0's first pixel, or a value no pixel has (every pixel then travels) -- decoded through the
+    assembly index: every frame equals the full-frame render, the device stream equals the host
+    reference byte for byte, and its device byte count is the stream's length."""
+    from atray_amd import shard as S
+    upload(eng, "Dragon", True)
+    W, H, F, world = 480, 270, 2, 3
+    cams = [E.camera(W, H, 1, 1, eye=(0.1 + 0.05 * f, 2.0, 0.0)) for f in range(F)]
+    plan = S.ShardPlan(W, H, world, 64)
+    off = S.frame_offsets(plan, F)
+    dst = torch.from_numpy(S.frames_assembly_index(plan, F)).cuda()
+    img = torch.zeros(F * W * H, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    bg = None
+    for r in range(world):
+        n = plan.sizes[r]
+        fb = torch.zeros(F * n, dtype=torch.int32, device="cuda")
+        fr = E.atr_frame(E.ATR_LAYOUT_PACKED, fb.data_ptr(), None, None, None, None, None)
+        eng.render_start_cameras(cams, plan.tiles[r], fr, n, SEED, stream=s)
+        torch.cuda.synchronize()
+        host = fb.cpu().numpy().view(np.uint32)
+        if bg is None:
+            bg = {"sky": S.background_value(host), "first": int(host[0]), "absent": 0x01000000}[bgsel]
+        out = torch.full((E.pack_bgr_masked_bound(F * n),), 0xA5, dtype=torch.uint8, device="cuda")
+        nbytes = torch.zeros(1, dtype=torch.int64, device="cuda")
+        eng.pack_bgr_masked(fb.data_ptr(), F * n, bg, out.data_ptr(), nbytes.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        want = S.pack_bgr_masked_host(host, bg)
+        assert int(nbytes.item()) == want.size
+        assert np.array_equal(out[:want.size].cpu().numpy(), want)
+        if bgsel == "sky":
+            assert want.size < 0.3 * 3 * F * n  # mostly sky: far below the 3-byte exchange
+        eng.scatter_bgr_masked(out.data_ptr(), F * n, dst[off[r]:].data_ptr(), img.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    for f in range(F):
+        full = run(eng, cams[f])
+        assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
+
+
 def test_block_cache_eviction_waits_for_every_stream(eng):
     """A tile list's cached block set read by launches on two streams is rewritten only after both
     have finished (round-2 advice: the slot's event once covered only the later stream): a long

@@ -183,3 +183,22 @@ def test_assembly_share():
     assert 0.1 < c3 < 0.2 and 0.0 < c4 < 0.001
     assert assembly_share(n, 0.0, 8) == 0.0 and assembly_share(n, 0.34, 1) == 0.0
     assert assembly_share(n, 1e-6, 8) == 0.5  # capped
+
+
+def test_masked_exchange_host_roundtrip():
+    """The masked exchange's host references (atr_pack_bgr_masked / atr_scatter_bgr_masked): any
+    background value, ragged chunk counts and empty input round-trip exactly, and the stream length
+    is header + chunk offsets + 1 KB of mask per 8192-pixel chunk + 3 B per non-background pixel."""
+    from atray_amd.shard import pack_bgr_masked_host, scatter_bgr_masked_host, background_value
+    rng = np.random.default_rng(7)
+    for n in (0, 1, 63, 64, 65, 8191, 8192, 8193, 70001):
+        bg = 0x007F664C
+        fb = np.where(rng.random(n) < 0.15, rng.integers(0, 1 << 24, n), bg).astype(np.uint32)
+        for b in (bg, background_value(fb), 0x01000000):
+            st = pack_bgr_masked_host(fb, b)
+            nc = -(-n // 8192)
+            assert st.size == 16 + 4 * nc + 1024 * nc + 3 * int((fb != b).sum())
+            perm = rng.permutation(n)
+            img = np.zeros(n, np.uint32)
+            scatter_bgr_masked_host(st, n, perm, img)
+            assert np.array_equal(img[perm], fb)
