@@ -187,7 +187,18 @@ int main(int argc, char** argv) {
     std::vector<int64_t> bytes_of(size_t(world), 0);
     uint8_t* d_enc = nullptr;
     if (exchange == "masked") {  // phase 1: each rank's stream length to rank 0
-        const uint32_t background = 0x004C667Fu;  // the sky: B 127, G 102, R 76 (any value is exact; this is the common one)
+        // the background: this rank's most common pixel (the sky's colour); any value is exact
+        uint32_t background = 0;
+        if (n) {
+            std::vector<uint32_t> px(static_cast<size_t>(n));
+            ATR(atr_memcpy_d2h(ctx, px.data(), d_fb, px.size() * 4));
+            std::sort(px.begin(), px.end());
+            size_t best = 0;
+            for (size_t i = 0, j; i < px.size(); i = j) {
+                for (j = i; j < px.size() && px[j] == px[i]; ++j) {}
+                if (j - i > best) { best = j - i; background = px[i]; }
+            }
+        }
         d_enc = dalloc<uint8_t>(ctx, size_t(atr_pack_bgr_masked_bound(n)));
         int64_t* d_nb = dalloc<int64_t>(ctx, 1);
         ATR(atr_pack_bgr_masked(ctx, d_fb, n, background, d_enc, d_nb, nullptr));
