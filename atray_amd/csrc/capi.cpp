@@ -46,6 +46,10 @@ extern "C" hipError_t atr_launch_plan(const atr::DBlock* base, int32_t nb, unsig
 extern "C" size_t atr_plan_work_bytes(int32_t nb);
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s);
 extern "C" int64_t atr_masked_chunks(int64_t n);
+extern "C" int64_t atr_masked_group_words(int64_t npixels);
+extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
+                                               const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
+                                               int64_t image_stride, uint32_t* goff, hipStream_t s);
 extern "C" hipError_t atr_launch_pack_bgr_masked(const uint32_t* src, int64_t n, uint32_t bg, uint8_t* out,
                                                  int64_t* nbytes, hipStream_t s);
 extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n, const int64_t* dst_index,
@@ -1826,6 +1830,28 @@ int atr_scatter_bgr_masked(atr_ctx* c, const uint8_t* packed, int64_t npixels, c
         return ATR_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(atr_launch_scatter_bgr_masked(packed, npixels, dst_index, image, static_cast<hipStream_t>(stream)));
+    return ATR_OK;
+}
+
+int atr_unpack_masked(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width, int32_t height,
+                      const uint8_t* packed, int32_t nframes, uint32_t* image, int64_t image_stride, void* stream) {
+    if (!c || !packed || !image || width <= 0 || height <= 0 || ntiles < 0 || (ntiles && !tiles) || nframes < 0 ||
+        image_stride < int64_t(width) * height)
+        return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ATR_OK;
+    BlockSet* bs = get_blocks(c, tiles, ntiles, width, height, rc);  // the render's cached set
+    if (!bs) return rc;
+    const int64_t own = bs->packed_pixels;
+    if (nframes == 0 || own == 0) return ATR_OK;
+    if (int64_t(nframes) * own >= (int64_t(1) << 32)) return ATR_E_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
+    void* goff = nullptr;
+    HIPCHK(hipMallocAsync(&goff, sizeof(uint32_t) * size_t(atr_masked_group_words(int64_t(nframes) * own)), s));
+    HIPCHK(atr_launch_unpack_masked(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed,
+                                    nframes, own, image, image_stride, static_cast<uint32_t*>(goff), s));
+    HIPCHK(hipFreeAsync(goff, s));
+    HIPCHK(note_launch(c, s, bs));
     return ATR_OK;
 }
 

@@ -27,7 +27,10 @@ constexpr float kInvU32Max = 2.328306437e-10F;    // PL_base_defs.h:75
 constexpr float kTol = 0.0001f;                   // ray.h:5
 constexpr int kMaskLevels = 16;                   // traversal mask-stack depth (8 bits/level)
 constexpr int kMaxMaterials = 32;
-constexpr int kMaxFrameCams = 16;  // distinct cameras per multi-frame launch (kernel argument)
+#ifndef ATR_MAX_FRAME_CAMS  // experiment builds: more cameras per launch (kernel argument size)
+#define ATR_MAX_FRAME_CAMS 16
+#endif
+constexpr int kMaxFrameCams = ATR_MAX_FRAME_CAMS;  // distinct cameras per multi-frame launch (kernel argument)
 constexpr int kMaxModels = 8;
 // Primitive slots per leaf cluster (atr_tuning.cluster_size <= this) and 16-B words per cluster
 // block (one 128-B line: record (2), screen normals (6)). 32 slots in 256-B blocks measured slower

@@ -7,6 +7,8 @@
 
 #include <stdint.h>
 
+#include "engine.h"
+
 namespace atr {
 
 // One pixel per lane; a wave's 64 pixels are 192 consecutive bytes (coalesced byte stores).
@@ -169,6 +171,55 @@ __global__ __launch_bounds__(256) void masked_scatter_kernel(const uint8_t* __re
     }
 }
 
+
+// Block-structured decode (atr_unpack_masked): the stream of a PACKED render of a tile list is in
+// its blocks' slot order, so each 8x8 block's wave finds its pixels' image positions from the block
+// record (32 B per 64 pixels) instead of an 8-B index per pixel. Each 64-slot group's first payload
+// pixel comes from a per-chunk scan of the mask popcounts (masked_group_offsets_kernel).
+__global__ __launch_bounds__(128) void masked_group_offsets_kernel(const uint8_t* __restrict__ in, int64_t nchunk,
+                                                                   uint32_t* __restrict__ goff) {
+    __shared__ uint32_t wsum[2];
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x, ln = t & 63, w = t >> 6;
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk) + c * (kMaskChunk / 32);
+    const uint32_t v = uint32_t(__popc(mw[2 * t]) + __popc(mw[2 * t + 1]));
+    uint32_t x = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = uint32_t(__shfl_up(int(x), d));
+        if (ln >= d) x += y;
+    }
+    if (ln == 63) wsum[w] = x;
+    __syncthreads();
+    goff[c * (kMaskChunk / 64) + t] = reinterpret_cast<const uint32_t*>(in + 16)[c] + (w ? wsum[0] : 0u) + x - v;
+}
+
+__global__ __launch_bounds__(256) void unpack_masked_kernel(const DBlock* __restrict__ blocks, int32_t nblocks,
+                                                            int32_t width, const uint8_t* __restrict__ in,
+                                                            int64_t nchunk, const uint32_t* __restrict__ goff,
+                                                            int32_t nframes, int64_t own, uint32_t* __restrict__ image,
+                                                            int64_t image_stride) {
+    const int64_t wv = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (wv >= int64_t(nblocks) * nframes) return;
+    const int32_t f = int32_t(wv / nblocks), b = int32_t(wv - int64_t(f) * nblocks);
+    const DBlock blk = blocks[b];
+    const uint64_t mask = uint64_t(blk.mask_lo) | (uint64_t(blk.mask_hi) << 32);
+    if (!((mask >> lane) & 1)) return;
+    const uint32_t bg = reinterpret_cast<const uint32_t*>(in)[1];
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk);
+    const uint8_t* pay = in + 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk;
+    const int64_t slot = int64_t(f) * own + blk.out_base + __popcll(mask & ((uint64_t(1) << lane) - 1));
+    const int64_t g = slot >> 6;
+    const int bit = int(slot & 63);
+    const uint64_t m = uint64_t(mw[2 * g]) | (uint64_t(mw[2 * g + 1]) << 32);
+    uint32_t v = bg;
+    if ((m >> bit) & 1) {
+        const uint8_t* s = pay + 3 * int64_t(goff[g] + uint32_t(__popcll(m & ((uint64_t(1) << bit) - 1))));
+        v = uint32_t(s[0]) | (uint32_t(s[1]) << 8) | (uint32_t(s[2]) << 16);
+    }
+    image[int64_t(f) * image_stride + int64_t(blk.y0 + (lane >> 3)) * width + blk.x0 + (lane & 7)] = v;
+}
+
 }  // namespace atr
 
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s) {
@@ -209,3 +260,19 @@ extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n
     hipLaunchKernelGGL(atr::masked_scatter_kernel, dim3(unsigned(nc)), dim3(256), 0, s, in, n, dst_index, image, nc);
     return hipGetLastError();
 }
+
+extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
+                                               const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
+                                               int64_t image_stride, uint32_t* goff, hipStream_t s) {
+    const int64_t nc = atr_masked_chunks(int64_t(nframes) * own);
+    if (nc <= 0 || nblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(atr::masked_group_offsets_kernel, dim3(unsigned(nc)), dim3(128), 0, s, in, nc, goff);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t waves = int64_t(nblocks) * nframes;
+    hipLaunchKernelGGL(atr::unpack_masked_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, s, blocks, nblocks,
+                       width, in, nc, goff, nframes, own, image, image_stride);
+    return hipGetLastError();
+}
+
+extern "C" int64_t atr_masked_group_words(int64_t npixels) { return atr_masked_chunks(npixels) * (atr::kMaskChunk / 64); }

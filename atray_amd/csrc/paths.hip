@@ -53,6 +53,16 @@ __device__ __forceinline__ void path_finish(float4_t* out, uint32_t o, V3 ret, u
     out[o] = float4_t{ret.x, ret.y, ret.z, __uint_as_float(casts)};
 }
 
+// Without AA every sample of a pixel casts the same camera ray (renderer.cpp:348-357), so when it
+// meets the sky every sample's path ends there with the same colour and no ray_casts. Then only
+// sample 0 writes its result slot, with this marker in place of the count (a real count is at most
+// the bounce limit), and the resolve takes that colour for every sample: c4 skips ~86% of the
+// camera kernel's result writes and of the resolve's reads; the sum is the same f32 adds.
+constexpr uint32_t kAllSky = 0xFFFFFFFFu;
+#ifndef ATR_SKY_ELIDE  // experiment builds: 0 = every sample writes its result slot (round 5)
+#define ATR_SKY_ELIDE 1
+#endif
+
 // Sort key of a queued ray (PathSort, engine.h): the octahedral cell of its direction (kSortDirs x
 // kSortDirs over the unfolded octahedron) and the Morton code of its origin's cell, b bits per axis
 // over the scene box, interleaved as below.
@@ -199,7 +209,8 @@ __global__ __launch_bounds__(256, OCC) void path_camera_kernel(PathParams P) {
         const DMaterial& mat = S->mats[id.material];
         if (id.type == T_SKY) {  // :225-229 at i = 0
             ret = add(ret, had(w, mk(mat.ex, mat.ey, mat.ez)));
-            path_finish(P.out, g, ret, 0u);
+            if (cm.anti_aliasing || !ATR_SKY_ELIDE) path_finish(P.out, g, ret, 0u);
+            else if (s == 0) path_finish(P.out, g, ret, kAllSky);  // the pixel's every sample (kAllSky)
         } else {
             bounce_shade(mat, id, o, d, ret, w, st, stream);  // :231-258
             if (bl <= 1) path_finish(P.out, g, ret, uint32_t(bl));  // ran to the limit (:260)
@@ -315,10 +326,15 @@ __global__ __launch_bounds__(256) void path_resolve_kernel(PathParams P) {
     const float4_t* src = P.out + int64_t(cellrel) * 64 * int64_t(spp) + lane;
     V3 col = mk(0.f, 0.f, 0.f);
     uint32_t casts = 0;
+    // sample 0 first: kAllSky = every sample of the pixel met the sky with this colour
+    const float4_t v0 = traced && spp > 0 ? src[0] : float4_t{0.f, 0.f, 0.f, 0.f};
+    const bool all_sky = traced && spp > 0 && !cm.anti_aliasing && __float_as_uint(v0.w) == kAllSky;
     for (uint32_t s = 0; s < spp; ++s) {  // col += cast_ray(...) in sample order (:353-356)
         V3 c = mk(0.f, 0.f, 0.f);
-        if (traced) {
-            const float4_t v = src[64 * int64_t(s)];
+        if (all_sky) {
+            c = mk(v0.x, v0.y, v0.z);
+        } else if (traced) {
+            const float4_t v = s == 0 ? v0 : src[64 * int64_t(s)];
             c = mk(v.x, v.y, v.z);
             casts += __float_as_uint(v.w);
         }

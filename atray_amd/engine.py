@@ -112,7 +112,7 @@ EXPORTS = [
     "atr_render_start_cameras", "atr_mesh_load_obj_threaded", "atr_mesh_parse_obj_threaded",
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_default_tuning", "atr_set_tuning", "atr_get_tuning", "atr_pack_bgr", "atr_scatter_bgr",
-    "atr_pack_bgr_masked_bound", "atr_pack_bgr_masked", "atr_scatter_bgr_masked",
+    "atr_pack_bgr_masked_bound", "atr_pack_bgr_masked", "atr_scatter_bgr_masked", "atr_unpack_masked",
     "atr_render_plan_info", "atr_workspace_info",
 ]
 # the diagnostic build's extra symbols (include/atray_diag.h; make -C atray_amd/csrc DIAG=1)
@@ -181,6 +181,7 @@ def lib():
         "atr_pack_bgr_masked_bound": ([i64], i64),
         "atr_pack_bgr_masked": ([vp, vp, i64, u32, vp, vp, vp], C.c_int),
         "atr_scatter_bgr_masked": ([vp, vp, i64, vp, vp, vp], C.c_int),
+        "atr_unpack_masked": ([vp, vp, i32, i32, i32, vp, i32, vp, i64, vp], C.c_int),
         "atr_render_simd_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
@@ -582,6 +583,14 @@ class Engine:
         check(lib().atr_scatter_bgr_masked(self.h, C.c_void_p(packed_ptr), int(npixels), C.c_void_p(index_ptr),
                                            C.c_void_p(image_ptr), C.c_void_p(stream) if stream else None),
               "scatter bgr masked")
+
+    def unpack_masked(self, tiles, width, height, packed_ptr, nframes, image_ptr, image_stride, stream=None):
+        """The masked stream of a PACKED render of `tiles` (nframes frames) into IMAGE frames
+        image_stride pixels apart (atr_unpack_masked: positions from the tile list's blocks)."""
+        arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
+        check(lib().atr_unpack_masked(self.h, C.cast(arr, C.c_void_p), n, int(width), int(height),
+                                      C.c_void_p(packed_ptr), int(nframes), C.c_void_p(image_ptr), int(image_stride),
+                                      C.c_void_p(stream) if stream else None), "unpack masked")
 
     def plan_info(self, tiles, width, height):
         """The single-frame plan of a tile list (diagnostic): (base index per planned block, masks

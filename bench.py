@@ -369,9 +369,9 @@ def main():
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.streams <= 0:
         args.streams = default_streams(args.config)
-    if args.frames_per_launch <= 0:
-        args.frames_per_launch = max(4 * max(world, args.sim_world), -(-args.steps // max(1, args.streams)))
-    args.frames_per_launch = max(1, min(16, args.frames_per_launch))
+    if args.frames_per_launch <= 0:  # the library's cap: 16 cameras per launch (kMaxFrameCams)
+        args.frames_per_launch = min(16, max(4 * max(world, args.sim_world), -(-args.steps // max(1, args.streams))))
+    args.frames_per_launch = max(1, min(32, args.frames_per_launch))  # explicit: experiment builds may allow more
     if args.selftest:
         return selftest(args)
     return run(args)
@@ -658,6 +658,7 @@ def run(args):
                 nsz = [torch.zeros(world, dtype=torch.int64, device="cpu" if on_host else dev) for _ in range(S_)]
                 dst_idx = torch.from_numpy(S.frames_assembly_index(plan, F_)).to(dev)
                 images = [torch.zeros(F_ * npx, dtype=torch.int32, device=dev) for _ in range(S_)]
+                rtiles = [E.tiles_array([list(t) for t in plan.tiles[r]]) if sizes[r] else None for r in range(world)]
         elif bgr:
             # 3-byte exchange: every rank packs its F frames into bytes (rank 0 straight into its
             # block of the byte gather buffer), rank 0 scatters the gathered bytes into the images
@@ -722,11 +723,10 @@ def run(args):
                 if rank == 0:
                     if on_host:
                         recv_dev[q].copy_(recv[q])
-                    for r in range(1, world):
+                    for r in range(1, world):  # positions from rank r's tile blocks (atr_unpack_masked)
                         if sizes[r]:
-                            eng.scatter_bgr_masked(recv_dev[q][int(roff[r]):].data_ptr(), nf * sizes[r],
-                                                   dst_idx[off[r]:].data_ptr(), images[q].data_ptr(),
-                                                   stream=streams[q].cuda_stream)
+                            eng.unpack_masked(rtiles[r], W, H, recv_dev[q][int(roff[r]):].data_ptr(), nf,
+                                              images[q].data_ptr(), npx, stream=streams[q].cuda_stream)
                     if own:
                         images[q].index_copy_(0, dst_idx[off[0]:off[0] + nf * own], fbs[q][:nf * own])
                 return
@@ -856,6 +856,10 @@ def run(args):
     launch_done = [round(ev0.elapsed_time(e), 3) for _, _, e in launch_ev]  # ms after the timed region's start
     launch_ms = [a.elapsed_time(e) for _, a, e in launch_ev]  # each timed launch's render, on its stream
     launch_frames = [nf for nf, _, _ in launch_ev]
+    stream_bpf = None  # this rank's masked stream bytes per frame (the last launch of each stream)
+    if masked and own and pr != 0:
+        js = sorted(launch_nf)[-S_:]
+        stream_bpf = round(sum(int(nbytes[j % S_].item()) for j in js) / max(1, sum(launch_nf[j] for j in js)))
     rays = torch.stack(traced).sum().reshape(1)
     local_rays_per_frame = float(rays.item()) / max(1, args.steps)  # this rank's traced rays per frame
     if world > 1:
@@ -980,7 +984,8 @@ def run(args):
                           "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),
                           "cell_plan": cell_split,
                           "shard_pixels": [int(x) for x in sizes]},
-               **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange"}} if sim else {}),
+               **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange",
+                           "stream_bytes_per_frame": stream_bpf}} if sim else {}),
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
         if steady:
             out["steady_state"] = steady

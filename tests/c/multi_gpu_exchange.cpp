@@ -7,7 +7,7 @@
 //       PACKED (atr_render_start)
 //   wait_for_render_from_camera_to_finish (:457-471) -> atr_render_wait; per-tile ray_casts
 //       (atr_packed_tile_ray_casts); the pixels and the tile sums to rank 0 (grouped ncclSend /
-//       ncclRecv), rank 0 assembles the framebuffer (atr_unpack, or atr_scatter_bgr_masked for the
+//       ncclRecv), rank 0 assembles the framebuffer (atr_unpack, or atr_unpack_masked for the
 //       masked exchange) and sums total_ray_casts (:465-468)
 //
 // usage: multi_gpu_exchange OBJ W H SPP BOUNCES [--exchange u32|masked] [--side S] [--out FILE]
@@ -239,15 +239,9 @@ int main(int argc, char** argv) {
         for (int r = 0; r < world; ++r) {
             const std::vector<atr_tile>& tr = tiles_of[size_t(r)];
             if (tr.empty()) continue;
-            if (exchange == "masked") {
-                std::vector<int64_t> map(static_cast<size_t>(n_of[size_t(r)]));
-                atr_packed_pixel_map(tr.data(), int32_t(tr.size()), W, H, map.data(), int64_t(map.size()));
-                int64_t* d_map = dalloc<int64_t>(ctx, map.size());
-                ATR(atr_memcpy_h2d(ctx, d_map, map.data(), sizeof(int64_t) * map.size()));
-                ATR(atr_scatter_bgr_masked(ctx, static_cast<const uint8_t*>(d_recv[size_t(r)]), n_of[size_t(r)], d_map,
-                                           d_image, nullptr));
-                ATR(atr_memcpy_d2h(ctx, map.data(), d_map, 8));  // orders the free after the decode
-                ATR(atr_device_free(ctx, d_map));
+            if (exchange == "masked") {  // positions from rank r's tile blocks
+                ATR(atr_unpack_masked(ctx, tr.data(), int32_t(tr.size()), W, H, static_cast<const uint8_t*>(d_recv[size_t(r)]),
+                                      1, d_image, int64_t(W) * H, nullptr));
             } else {
                 ATR(atr_unpack(ctx, tr.data(), int32_t(tr.size()), W, static_cast<const uint32_t*>(d_recv[size_t(r)]),
                                d_image, nullptr));

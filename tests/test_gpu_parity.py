@@ -610,7 +610,7 @@ def test_bgr_exchange_reassembles_frames(eng):
 
 @pytest.mark.parametrize("bgsel", ["sky", "first", "absent"])
 def test_masked_exchange_reassembles_frames(eng, bgsel):
-    """The masked exchange (atr_pack_bgr_masked / atr_scatter_bgr_masked, round 6): 3 ranks' packed
+    """The masked exchange (atr_pack_bgr_masked / atr_scatter_bgr_masked / atr_unpack_masked, round 6): 3 ranks' packed
     shard frames (2 per launch) encoded against a background value -- the frame's common sky value,
     rank 0's first pixel, or a value no pixel has (every pixel then travels) -- decoded through the
     assembly index: every frame equals the full-frame render, the device stream equals the host
@@ -623,6 +623,7 @@ def test_masked_exchange_reassembles_frames(eng, bgsel):
     off = S.frame_offsets(plan, F)
     dst = torch.from_numpy(S.frames_assembly_index(plan, F)).cuda()
     img = torch.zeros(F * W * H, dtype=torch.int32, device="cuda")
+    img2 = torch.full((F * (W * H + 5),), 0x7F7F7F7F, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     bg = None
     for r in range(world):
@@ -644,10 +645,15 @@ def test_masked_exchange_reassembles_frames(eng, bgsel):
         if bgsel == "sky":
             assert want.size < 0.3 * 3 * F * n  # mostly sky: far below the 3-byte exchange
         eng.scatter_bgr_masked(out.data_ptr(), F * n, dst[off[r]:].data_ptr(), img.data_ptr(), stream=s)
+        # and straight from the tile list's blocks (atr_unpack_masked), frames W * H + 5 apart
+        eng.unpack_masked(plan.tiles[r], W, H, out.data_ptr(), F, img2.data_ptr(), W * H + 5, stream=s)
     torch.cuda.synchronize()
     for f in range(F):
         full = run(eng, cams[f])
         assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
+        o = f * (W * H + 5)
+        assert np.array_equal(img2[o:o + W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
+        assert (img2[o + W * H:o + W * H + 5] == 0x7F7F7F7F).all()
 
 
 def test_block_cache_eviction_waits_for_every_stream(eng):

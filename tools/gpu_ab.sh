@@ -2,6 +2,7 @@
 # A/B of the product library against experiments, general form: variants "prod", "exp=<name>" (atray_amd/_lib/exp/<name>.so) or
 # "tune=<k=v,...>" (product library, bench.py --tuning), "exp=<name>@<k=v,...>" (both) or
 # "args=<arg>+<arg>..." (product library, these bench.py arguments, e.g. args=--streams=1),
+# "expargs=<name>:<arg>+<arg>..." (an experiment build with bench.py arguments),
 # interleaved twice, on the configs given.
 # usage: gpu_ab.sh OUTDIR "variant ..." "c3 c4" [tests]
 set -o pipefail
@@ -29,6 +30,7 @@ for i in 1 2; do
       exp=*) L=atray_amd/_lib/exp/${v#exp=}.so;;
       tune=*) T="--tuning ${v#tune=}";;
       args=*) T=$(echo ${v#args=} | tr '+' ' ');;
+      expargs=*) x=${v#expargs=}; L=atray_amd/_lib/exp/${x%%:*}.so; T=$(echo ${x#*:} | tr '+' ' ');;
     esac
     for cfg in $3; do
       case $cfg in
