@@ -28,7 +28,7 @@ constexpr float kTol = 0.0001f;                   // ray.h:5
 constexpr int kMaskLevels = 16;                   // traversal mask-stack depth (8 bits/level)
 constexpr int kMaxMaterials = 32;
 #ifndef ATR_MAX_FRAME_CAMS  // experiment builds: more cameras per launch (kernel argument size)
-#define ATR_MAX_FRAME_CAMS 16
+#define ATR_MAX_FRAME_CAMS 24
 #endif
 constexpr int kMaxFrameCams = ATR_MAX_FRAME_CAMS;  // distinct cameras per multi-frame launch (kernel argument)
 constexpr int kMaxModels = 8;

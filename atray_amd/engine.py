@@ -480,7 +480,7 @@ class Engine:
 
     def render_start_cameras(self, cams, tiles, frame: atr_frame, frame_stride, seed, stream=None,
                              variant=ATR_KERNEL_AUTO):
-        """len(cams) frames (at most 16) in one launch, frame f from cams[f]; outputs frame_stride apart."""
+        """len(cams) frames (at most 24) in one launch, frame f from cams[f]; outputs frame_stride apart."""
         arr, n = tiles if isinstance(tiles, tuple) else tiles_array(tiles)
         ca = (atr_camera * len(cams))(*cams)
         check(lib().atr_render_start_cameras(self.h, C.cast(ca, C.c_void_p), len(cams), C.cast(arr, C.c_void_p), n,

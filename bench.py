@@ -63,12 +63,17 @@ GOLDEN_COUNTERS = {"c3": "dragon_1920x1080_tree", "c2": "monkey_1280x720_bf", "c
 MATERIALS = [((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0.5, 0.0), 0.3)]  # app.cpp:91-105
 
 
-def default_streams(config):
-    """Launches in flight by default: two for the 1-spp configs (one launch's tail hides behind the
-    other's work), one for the path-engine configs (two concurrent launches share the caches the
-    sorted bounce queues rely on)."""
+MAX_FRAME_CAMS = 24  # cameras per atr_render_start_cameras launch (the library's kMaxFrameCams)
+
+
+def default_streams(config, steps=0):
+    """Launches in flight by default: one for the path-engine configs (two concurrent launches
+    share the caches the sorted bounce queues rely on); for the 1-spp configs one
+    when a single launch holds every timed frame (its cells graded heaviest first across all the
+    frames: the driver's 20 c3 frames +3.6% over 10 + 10 on two streams, round 6), else two (one
+    launch's tail hides behind the other's work)."""
     spp, bounces = CONFIGS[config][3:5]
-    return 1 if (spp > 1 or bounces > 1) else 2
+    return 1 if (spp > 1 or bounces > 1 or steps <= MAX_FRAME_CAMS) else 2
 
 
 def orbit_eye(k):
@@ -319,7 +324,7 @@ def main():
                          "two concurrent launches share the caches that the sorted bounce queues rely on, "
                          "DESIGN.md §4h)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
-                    help="frames per launch (atr_render_start_cameras, at most 16); 1 = one frame per launch; "
+                    help="frames per launch (atr_render_start_cameras, at most MAX_FRAME_CAMS = 24); 1 = one frame per launch; "
                          "0 = the K steps in as few launches per stream as the cap allows, at least 4 x ranks "
                          "(a launch boundary inside a stream and the last launch's tail are the overheads)")
     ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
@@ -368,9 +373,10 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.streams <= 0:
-        args.streams = default_streams(args.config)
-    if args.frames_per_launch <= 0:  # the library's cap: 16 cameras per launch (kMaxFrameCams)
-        args.frames_per_launch = min(16, max(4 * max(world, args.sim_world), -(-args.steps // max(1, args.streams))))
+        args.streams = default_streams(args.config, args.steps)
+    if args.frames_per_launch <= 0:  # the library's cap: MAX_FRAME_CAMS cameras per launch
+        args.frames_per_launch = min(MAX_FRAME_CAMS, max(4 * max(world, args.sim_world),
+                                                         -(-args.steps // max(1, args.streams))))
     args.frames_per_launch = max(1, min(32, args.frames_per_launch))  # explicit: experiment builds may allow more
     if args.selftest:
         return selftest(args)

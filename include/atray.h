@@ -270,7 +270,7 @@ int atr_render_start_frames(atr_ctx* ctx, const atr_camera* cam, const atr_tile*
                             const atr_frame* frame, int32_t nframes, int64_t frame_stride, uint64_t seed,
                             void* stream, int32_t variant);
 /* The same with one camera per frame (an animation, a camera path): frame f renders cams[f]
-   (1 <= nframes <= 16). All cameras must share width, height, samples_per_pixel, bounce_limit
+   (1 <= nframes <= 24). All cameras must share width, height, samples_per_pixel, bounce_limit
    and anti_aliasing (ATR_E_INVALID otherwise); eye, facing and field of view may differ. Every
    frame equals atr_render_start_ex's output for its camera. */
 int atr_render_start_cameras(atr_ctx* ctx, const atr_camera* cams, int32_t nframes, const atr_tile* tiles,

@@ -80,5 +80,8 @@ def test_path_dispatches_count_the_queue_sort():
 
 
 def test_streams_default_per_config():
-    """bench.py --streams 0 (default): two for the 1-spp configs, one for the path-engine configs."""
-    assert {c: bench.default_streams(c) for c in bench.CONFIGS} == {"c1": 2, "c2": 2, "c3": 2, "c4": 1, "c5": 1}
+    """bench.py --streams 0 (default): one for the path-engine configs; for the 1-spp configs one
+    while a single launch holds every timed frame (the driver's 20), else two."""
+    assert {c: bench.default_streams(c, 20) for c in bench.CONFIGS} == {"c1": 1, "c2": 1, "c3": 1, "c4": 1, "c5": 1}
+    assert {c: bench.default_streams(c, 48) for c in bench.CONFIGS} == {"c1": 2, "c2": 2, "c3": 2, "c4": 1, "c5": 1}
+    assert bench.launch_sizes(20, bench.MAX_FRAME_CAMS, 1) == [20]

@@ -242,7 +242,7 @@ def test_per_frame_cameras_reject_mismatched_settings(eng):
     fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, None, None)
     with pytest.raises(E.AtrError):
         eng.render_start_cameras([a, b], [[0, 0, W - 1, H - 1]], fr, W * H, SEED)
-    with pytest.raises(E.AtrError):  # more than 16 cameras in one launch
-        big = torch.zeros(17 * W * H, dtype=torch.int32, device="cuda")
+    with pytest.raises(E.AtrError):  # more than 24 cameras in one launch
+        big = torch.zeros(25 * W * H, dtype=torch.int32, device="cuda")
         fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, big.data_ptr(), None, None, None, None, None)
-        eng.render_start_cameras([a] * 17, [[0, 0, W - 1, H - 1]], fr, W * H, SEED)
+        eng.render_start_cameras([a] * 25, [[0, 0, W - 1, H - 1]], fr, W * H, SEED)

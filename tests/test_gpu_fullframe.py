@@ -116,37 +116,40 @@ def test_c5_whole_frame_matches_oracle(eng):
     check_frame("c5", host_frame(o, 0, 3840, 2160), int(o["traced"].item()))
 
 
-def test_c3_timed_frames_match_oracle(eng):
-    """The driver's timed c3 frames (orbit positions 5..24) in the bench's timed shape: two
-    10-camera atr_render_start_cameras launches in flight on two streams through AUTO (the
-    7-wave HYBRID primary kernel), with the graded cell order calibrated on orbit frames 2-4
-    (bench.py run()); then each frame alone (the single-frame kernel and plan). Every frame
-    equals the oracle's, pixel for pixel."""
+@pytest.mark.parametrize("shape", ["one_launch", "two_streams"])
+def test_c3_timed_frames_match_oracle(eng, shape):
+    """The driver's timed c3 frames (orbit positions 5..24) in the bench's timed shape through AUTO
+    (the 7-wave HYBRID primary kernel), with the graded cell order calibrated on orbit frames 2-4
+    (bench.py run()): one atr_render_start_cameras launch of all 20 cameras (the default since
+    round 6), or two 10-camera launches in flight on two streams (round 5's shape); then each
+    frame alone (the single-frame kernel and plan). Every frame equals the oracle's, pixel for
+    pixel."""
     import bench
     from atray_amd import shard as S
-    W, H, F = 1920, 1080, 10
+    W, H = 1920, 1080
     n = W * H
     ks = list(range(5, 25))
+    groups = [ks] if shape == "one_launch" else [ks[:10], ks[10:]]
     cams = {k: E.camera(W, H, 1, 1, eye=bench.orbit_eye(k), facing=bench.APP_FACING) for k in ks}
     cc = sum(eng.cell_costs(E.camera(W, H, 1, 1, eye=bench.orbit_eye(k), facing=bench.APP_FACING), SEED)
              for k in (2, 3, 4))
     eng.set_cell_plan(W, H, S.graded_cell_plan(cc))
     try:
-        streams = [torch.cuda.Stream(torch.device("cuda", 0)) for _ in range(2)]
-        outs = [outputs(n, F) for _ in range(2)]
+        streams = [torch.cuda.Stream(torch.device("cuda", 0)) for _ in groups]
+        outs = [outputs(n, len(g)) for g in groups]
         torch.cuda.synchronize()
-        for q in range(2):
-            eng.render_start_cameras([cams[k] for k in ks[q * F:(q + 1) * F]], [[0, 0, W - 1, H - 1]],
-                                     frame_ptrs(outs[q]), n, SEED, stream=streams[q].cuda_stream)
+        for q, g in enumerate(groups):
+            eng.render_start_cameras([cams[k] for k in g], [[0, 0, W - 1, H - 1]], frame_ptrs(outs[q]), n, SEED,
+                                     stream=streams[q].cuda_stream)
         assert eng.wait()[0] == 0
         torch.cuda.synchronize()
-        for q in range(2):
-            assert int(outs[q]["traced"].item()) == sum(GOLD[f"c3_orbit{k}"]["traced"] for k in ks[q * F:(q + 1) * F])
-            for f in range(F):
-                check_frame(f"c3_orbit{ks[q * F + f]}", host_frame(outs[q], f, W, H))
+        for q, g in enumerate(groups):
+            assert int(outs[q]["traced"].item()) == sum(GOLD[f"c3_orbit{k}"]["traced"] for k in g)
+            for f, k in enumerate(g):
+                check_frame(f"c3_orbit{k}", host_frame(outs[q], f, W, H))
     finally:
         eng.set_cell_plan(W, H, None)
-    for k in ks:
-        o = render_one(eng, cams[k], E.ATR_KERNEL_AUTO)
-        check_frame(f"c3_orbit{k}", host_frame(o, 0, W, H), int(o["traced"].item()))
-
+    if shape == "one_launch":
+        for k in ks:
+            o = render_one(eng, cams[k], E.ATR_KERNEL_AUTO)
+            check_frame(f"c3_orbit{k}", host_frame(o, 0, W, H), int(o["traced"].item()))
