@@ -192,6 +192,9 @@ int32_t default_parse_threads() {
     const unsigned hw = std::thread::hardware_concurrency();
     return int32_t(std::max(1u, std::min(16u, hw)));
 }
+#ifndef ATR_MAX_BATCH_LOG2  // experiment builds: 29 to study the 2^29-path cliff
+#define ATR_MAX_BATCH_LOG2 28
+#endif
 #ifndef ATR_PATH_SPLIT_DEFAULT
 #define ATR_PATH_SPLIT_DEFAULT 0
 #endif
@@ -1030,7 +1033,7 @@ int atr_set_tuning(atr_ctx* c, const atr_tuning* t) {
     if (!c || !t) return ATR_E_INVALID;
     if (t->xcd_chunk < 0 || t->xcd_chunk > 4096 || t->frame_rotate < 0 || t->frame_rotate > 1024 ||
         t->hybrid_a < -4096 || t->hybrid_a > 4096 || t->hybrid_b < -4096 || t->hybrid_b > 4096 ||
-        t->path_batch_log2 < 12 || t->path_batch_log2 > 28 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
+        t->path_batch_log2 < 12 || t->path_batch_log2 > ATR_MAX_BATCH_LOG2 || t->cluster_size < 1 || t->cluster_size > kMaxClusterSize ||
         t->frame_plan < 0 || t->frame_plan > 1 || (t->path_camera_occ != 0 && (t->path_camera_occ < 5 || t->path_camera_occ > 7)) ||
         (t->path_bounce_occ != 0 && (t->path_bounce_occ < 5 || t->path_bounce_occ > 7)) ||
         (t->primary_occ != 0 && (t->primary_occ < 6 || t->primary_occ > 8)) ||

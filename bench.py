@@ -66,14 +66,16 @@ MATERIALS = [((0.3, 0.4, 0.5), (0.2, 0.3, 0.4), 0.3), ((0.4, 0.2, 0.2), (0.92, 0
 MAX_FRAME_CAMS = 24  # cameras per atr_render_start_cameras launch (the library's kMaxFrameCams)
 
 
-def default_streams(config, steps=0):
+def default_streams(config, steps=0, world=1):
     """Launches in flight by default: one for the path-engine configs (two concurrent launches
-    share the caches the sorted bounce queues rely on); for the 1-spp configs one
-    when a single launch holds every timed frame (its cells graded heaviest first across all the
-    frames: the driver's 20 c3 frames +3.6% over 10 + 10 on two streams, round 6), else two (one
-    launch's tail hides behind the other's work)."""
+    share the caches the sorted bounce queues rely on); for the 1-spp configs on one
+    GPU, one when a single launch holds every timed frame (its cells graded heaviest first across
+    all the frames: the driver's 20 c3 frames +2.5-3.6% over 10 + 10 on two streams, round 6), else
+    two (one launch's tail hides behind the other's work); with N > 1 shards two (stream 0 at high
+    priority: its launch and exchange finish while the other renders; the 8-way c3 projection
+    4.98-5.12x against 4.45-4.58x for one launch)."""
     spp, bounces = CONFIGS[config][3:5]
-    return 1 if (spp > 1 or bounces > 1 or steps <= MAX_FRAME_CAMS) else 2
+    return 1 if (spp > 1 or bounces > 1 or (world <= 1 and steps <= MAX_FRAME_CAMS)) else 2
 
 
 def orbit_eye(k):
@@ -373,7 +375,7 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.streams <= 0:
-        args.streams = default_streams(args.config, args.steps)
+        args.streams = default_streams(args.config, args.steps, max(world, args.sim_world))
     if args.frames_per_launch <= 0:  # the library's cap: MAX_FRAME_CAMS cameras per launch
         args.frames_per_launch = min(MAX_FRAME_CAMS, max(4 * max(world, args.sim_world),
                                                          -(-args.steps // max(1, args.streams))))

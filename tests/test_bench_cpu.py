@@ -85,3 +85,4 @@ def test_streams_default_per_config():
     assert {c: bench.default_streams(c, 20) for c in bench.CONFIGS} == {"c1": 1, "c2": 1, "c3": 1, "c4": 1, "c5": 1}
     assert {c: bench.default_streams(c, 48) for c in bench.CONFIGS} == {"c1": 2, "c2": 2, "c3": 2, "c4": 1, "c5": 1}
     assert bench.launch_sizes(20, bench.MAX_FRAME_CAMS, 1) == [20]
+    assert {c: bench.default_streams(c, 20, 8) for c in bench.CONFIGS} == {"c1": 2, "c2": 2, "c3": 2, "c4": 1, "c5": 1}

@@ -2,7 +2,7 @@
 # Round 6: every rank's shard of the N-way cost plans (N = 2, 4, 8) alone on one GPU, in the same
 # timed shape as the full-frame line (bench.py --sim-world N --sim-rank r: render, per-tile
 # counters and the masked stream's encoding, as that rank runs them), for tools/project_r6.py.
-# usage: gpu_r6_sim.sh OUTDIR "c3 c4 c5" ["2 4 8"] [reps]
+# usage: gpu_r6_sim.sh OUTDIR "c3 c4 c5" ["2 4 8"] [reps] [extra bench.py args, e.g. "--streams 2"]
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/$1
@@ -21,9 +21,9 @@ for cfg in $2; do
     c4) A="--config c4 --steps 8 --warmup 2"; T=300;;
     c5) A="--config c5 --steps 2 --warmup 1"; T=600;;
   esac
-  run ${cfg}_full_$i $T $A
+  run ${cfg}_full_$i $T $A $5
   for w in ${3:-2 4 8}; do
-    for r in $(seq 0 $((w - 1))); do run ${cfg}_sim${w}_r${r}_$i $T $A --sim-world $w --sim-rank $r; done
+    for r in $(seq 0 $((w - 1))); do run ${cfg}_sim${w}_r${r}_$i $T $A --sim-world $w --sim-rank $r $5; done
   done
 done
 done
