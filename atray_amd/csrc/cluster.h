@@ -41,6 +41,13 @@ __device__ __forceinline__ void load_prim(const DModel& m, uint32_t k, float4_t&
 
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
 
+// Which scan flavours load the first screen normals with the box test (cluster_cands EARLY): bit 0
+// primary-only rays, bit 1 camera rays of the path engine, bit 2 bounce rays (experiment builds
+// set others; 0 = every flavour loads them after the box test passes)
+#ifndef ATR_EARLY_NRM
+#define ATR_EARLY_NRM 7
+#endif
+
 // Ray-side constants of the cluster screen, once per ray (f16 direction, its L1 norm).
 struct ScreenRay {
     float ax, ay, az, sd;
@@ -155,7 +162,7 @@ __device__ __forceinline__ uint32_t screen8(const ScreenRay& sr, float blo, floa
 
 // Cluster c of a leaf: the padded box tests and the screen against the bound `best`. Returns the
 // mask of the primitives (slot 16 c + bit) that still need the full test.
-template <bool COUNT>
+template <bool COUNT, bool EARLY = true>
 __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m, uint32_t c, float4_t lo, float4_t hi,
                                                   float best, Ctr& ct) {
     // the screen constants (7 values) are recomputed for every cluster from an opaque copy of the
@@ -164,11 +171,18 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
     Ray rr = r;
     asm volatile("" : "+v"(rr.d.x), "+v"(rr.d.y), "+v"(rr.d.z), "+v"(rr.inv.x), "+v"(rr.inv.y), "+v"(rr.inv.z));
     const ScreenRay sr = screen_ray(rr);
+    const uint4_t* nb = m.cnrm + kClusterBlock * size_t(c);
+    // EARLY: the first 8 slots' screen normals are loaded together with the box test instead of
+    // after it passes -- one dependent memory round trip less per cluster on the dealt rounds' chain,
+    // at 12 VGPRs held through the pads (c3 +1.2%, c4 +0.7%, round 6)
+    uint4_t e0, e1, ez;
+    if constexpr (EARLY) {
+        e0 = nb[0], e1 = nb[1], ez = nb[kMaxClusterSize / 4];
+    }
     float dlo, dhi;
     if (!cluster_pads(r, sr, lo, hi, best, dlo, dhi)) return 0;
     const uint32_t n = (__float_as_uint(lo.w) & 31u) + 1u;
     if constexpr (COUNT) ct.screen += n;
-    const uint4_t* nb = m.cnrm + kClusterBlock * size_t(c);
     const uint32_t slots = (2u << (n - 1)) - 1u;  // [0, n), 1 <= n <= 16
     const float q = hi.w;
     if (!(q >= 1.1754944e-38f)) return slots;  // zero or subnormal step (degenerate normals): no screen
@@ -185,8 +199,13 @@ __device__ __forceinline__ uint32_t cluster_cands(const Ray& r, const DModel& m,
 #ifndef ATR_SCREEN_TWO_CMP
     float mid, half;
     screen_band(blo, ahi, mid, half);
-    for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
-        cand |= screen8(sr, -mid, half, nb[g / 4], nb[g / 4 + 1], nb[kMaxClusterSize / 4 + g / 8]) << g;
+    if constexpr (EARLY) {
+        cand = screen8(sr, -mid, half, e0, e1, ez);
+        if (n > 8) cand |= screen8(sr, -mid, half, nb[2], nb[3], nb[kMaxClusterSize / 4 + 1]) << 8;
+    } else {
+        for (uint32_t g = 0; g < n; g += 8)  // eight primitives per step: (nx, ny) x 8, nz x 8
+            cand |= screen8(sr, -mid, half, nb[g / 4], nb[g / 4 + 1], nb[kMaxClusterSize / 4 + g / 8]) << g;
+    }
 #else
     for (uint32_t g = 0; g < n; g += 8)
         cand |= screen8(sr, blo, ahi, nb[g / 4], nb[g / 4 + 1], nb[kMaxClusterSize / 4 + g / 8]) << g;

@@ -260,6 +260,9 @@ __global__ __launch_bounds__(256) void plan_order_kernel(const DBlock* __restric
             t.mask_lo = uint32_t(m & band);
             t.mask_hi = uint32_t((m & band) >> 32);
             t.out_base = ob;
+#ifdef ATR_PLAN_PRIO_CLASSES  // experiment: the heaviest classes' waves at raised issue priority
+            if (k < ATR_PLAN_PRIO_CLASSES) t.flags |= kBlockPrio;
+#endif
             ob += __popcll(m & band);
             out[s + p] = t;
         }

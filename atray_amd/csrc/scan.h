@@ -405,6 +405,8 @@ template <bool COUNT, bool HYB, bool UO, bool NUV, int K = kLeafBuf>
 __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, int w, int ln, bool live, FlatQ& q,
                                                Ctr& ct, int32_t hyb_a, int32_t hyb_b) {
     FlatLds<K, !NUV>& L = flat_lds<K, !NUV>();
+    // flavour of the scan (primary-only, camera, bounce rays) -> early screen normals (cluster.h)
+    constexpr bool kEarly = ((NUV ? 1 : UO ? 2 : 4) & ATR_EARLY_NRM) != 0;
     ATR_PCLK(const uint64_t tc2 = clock64());
     uint32_t cf = 0, cn = 0;
     if (live) {
@@ -433,7 +435,7 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
             if (i < cn) {
                 const uint32_t c = cf + i;
                 const float bound = __uint_as_float(uint32_t(L.key[w][ln] >> 32));
-                cm = cluster_cands<COUNT>(r, m, c, m.clus[kClusterBlock * size_t(c)],
+                cm = cluster_cands<COUNT, kEarly>(r, m, c, m.clus[kClusterBlock * size_t(c)],
                                           m.clus[kClusterBlock * size_t(c) + 1], bound, ct);
             }
             cand_rounds<COUNT, UO, NUV, true, K>(r, m, w, ln, cm, kMaxClusterSize * (cf + i), ln, ct);
@@ -464,7 +466,7 @@ __device__ __forceinline__ void flat_leaf_step(const Ray& r, const DModel& m, in
         uint32_t cm = 0;
         if (valid) {
             const float bound = __uint_as_float(uint32_t(L.key[w][own] >> 32));
-            cm = cluster_cands<COUNT>(qr, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1],
+            cm = cluster_cands<COUNT, kEarly>(qr, m, c, m.clus[kClusterBlock * size_t(c)], m.clus[kClusterBlock * size_t(c) + 1],
                                       bound, ct);
         }
         cand_rounds<COUNT, UO, NUV, false, K>(r, m, w, ln, cm, kMaxClusterSize * c, own, ct);
