@@ -43,9 +43,11 @@ typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
 
 // Which scan flavours load the first screen normals with the box test (cluster_cands EARLY): bit 0
 // primary-only rays, bit 1 camera rays of the path engine, bit 2 bounce rays (experiment builds
-// set others; 0 = every flavour loads them after the box test passes)
+// set others; 0 = every flavour loads them after the box test passes). Not the camera rays: their
+// 6-wave kernel then spills 20 dwords instead of 5 and writes 4 GB more per c4 frame, for no time
+// measured (c4 3,824-3,826 Mrays/s without, 3,828-3,834 with)
 #ifndef ATR_EARLY_NRM
-#define ATR_EARLY_NRM 7
+#define ATR_EARLY_NRM 5
 #endif
 
 // Ray-side constants of the cluster screen, once per ray (f16 direction, its L1 norm).
