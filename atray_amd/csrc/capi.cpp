@@ -513,7 +513,7 @@ size_t sort_bytes(int64_t cap, int64_t bins) {
     return size_t(cap) * 12 + size_t(bins) * 8 + size_t(bins / kSortChunk) * 4;
 }
 
-hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels, int64_t sort_bins,
+hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int64_t grow_to, int32_t levels, int64_t sort_bins,
                           atr_ctx::PathWS*& out) {
     atr_ctx::PathWS* ws = nullptr;
     hipError_t e;
@@ -539,7 +539,8 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
         if ((e = hipEventSynchronize(ws->ev)) != hipSuccess) return e;
         if (ws->mem.p && (e = hipFree(ws->mem.p)) != hipSuccess) return e;
         ws->mem = DevBuf();
-        const int64_t ncap = std::max(ws->cap, cap);
+        // a workspace that already held paths and is too small grows to grow_to (a full batch)
+        int64_t ncap = std::max(ws->cap, ws->cap > 0 && ws->cap < cap ? std::max(cap, grow_to) : cap);
         const int32_t nlev = std::max(ws->levels, levels);
         const int64_t nbins = std::max(ws->sort_bins, sort_bins);
         ws->cap = 0;
@@ -547,9 +548,18 @@ hipError_t path_workspace(atr_ctx* c, hipStream_t s, int64_t cap, int32_t levels
         ws->sort_bins = 0;
         // 2 queues x kPathPlanes planes + the per-path results, 16 B per entry; the level counters;
         // the queue-sort buffers
-        const size_t bytes = nbins ? sort_offset(ncap, nlev) + sort_bytes(ncap, nbins)
-                                   : size_t(ncap) * 16 * (2 * kPathPlanes + 1) + size_t(nlev) * sizeof(PathCtl);
+        auto bytes_for = [&](int64_t n) {
+            return nbins ? sort_offset(n, nlev) + sort_bytes(n, nbins)
+                         : size_t(n) * 16 * (2 * kPathPlanes + 1) + size_t(nlev) * sizeof(PathCtl);
+        };
+        size_t bytes = bytes_for(ncap);
         e = hipMalloc(&ws->mem.p, bytes);
+        if (e == hipErrorOutOfMemory && ncap > cap) {  // the full batch does not fit: this launch's size
+            (void)hipGetLastError();
+            ncap = cap;
+            bytes = bytes_for(ncap);
+            e = hipMalloc(&ws->mem.p, bytes);
+        }
         if (e == hipErrorOutOfMemory) {
             (void)hipGetLastError();
             for (auto& w : c->path_ws)
@@ -599,14 +609,13 @@ hipError_t launch_paths_range(atr_ctx* c, const RenderParams& P, hipStream_t s, 
         for (int32_t lg = c->tune.path_batch_log2; lg >= 16 && e == hipErrorOutOfMemory; --lg) {
             const int64_t batch = std::max<int64_t>(1, (int64_t(1) << lg) / per_cell);
             cells = std::min<int64_t>(batch, cend - cbeg);
-            // capacity: this launch's batch rounded up to a power of two (at most a full batch), so a
-            // one-frame launch already holds the batch of the multi-frame launches that follow it
-            // capacity: this launch's paths rounded up to 2^20 (at most a full batch): a one-frame c4
-            // launch holds its 132.7 M paths (20.7 GB), not a whole 2^28 batch; a later launch that
-            // needs more regrows the workspace once
-            const int64_t need = cells * per_cell, gran = int64_t(1) << 20;
+            // capacity: this launch's paths rounded up to 2^24 (at most a full batch): a one-frame c4
+            // launch holds its 132.7 M paths (21 GB), not a whole 2^28 batch; a workspace that has to
+            // grow grows to a full batch at once, so a stream regrows at most once (a regrow inside a
+            // timed multi-frame run once measured a 4x slower c4 line, round 6)
+            const int64_t need = cells * per_cell, gran = int64_t(1) << 24;
             const int64_t cap = std::max(need, std::min((need + gran - 1) / gran * gran, batch * per_cell));
-            e = path_workspace(c, s, cap, std::max(levels, 8), bins, ws);
+            e = path_workspace(c, s, cap, std::max(batch * per_cell, cap), std::max(levels, 8), bins, ws);
             if (e == hipSuccess && ws->cap < cap) e = hipErrorOutOfMemory;
         }
         if (e != hipErrorOutOfMemory || sort_bits == 0) break;

@@ -168,8 +168,9 @@ typedef struct {
     int32_t path_batch_log2; /* PATHS: paths per batch = 2^this (the path queues hold one batch,
                                144 B per path, 156 with the queue sort), 12..28; default 28
                                (1920x1080 at 64 spp: a frame in one batch). A workspace holds the
-                               launch's paths rounded up to 2^20, at most one batch: 20.7 GB for a
-                               1920x1080 64-spp frame, 42 GB at most (4 per context: 167 GB).
+                               launch's paths rounded up to 2^24, at most one batch: 20.9 GB for a
+                               1920x1080 64-spp frame, 42 GB at most (4 per context: 167 GB);
+                               a workspace too small for a later launch grows to a whole batch.
                                2^29 measured 5-7x slower */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
     int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
