@@ -50,6 +50,43 @@ class ShardPlan:
         owner = E.balance_shard_tiles(width, height, side, world, costs, extra)
         return cls(width, height, world, side, owner, costs if heavy_first else None)
 
+    @classmethod
+    def curve(cls, costs, width: int, height: int, world: int, side: int = 64, rank0_extra: float = 0.0,
+              heavy_first: bool = True):
+        """Compact shards by recursive cost bisection: a group of ranks' tiles are cut across their
+        bounding box's longer side (tiles in column-major order for a vertical cut, row-major for a
+        horizontal one) where the first half of the ranks' share of the measured cost is reached,
+        each half recursing on its ranks; rank 0's share is short by rank0_extra x the mean load.
+        Each rank's tiles form a near-rectangle (one step at the cut), so its rays walk a compact
+        part of the scene (its caches hold less of the tree than under the longest-first deal,
+        whose tiles spread over the frame); the balance is within about one tile's cost per cut."""
+        costs = np.asarray(costs, np.int64)
+        grid = E.shard_grid(width, height, side)
+        total = float(costs.sum())
+        extra = rank0_extra * total / max(1, world)
+        want = np.full(world, (total + extra) / max(1, world))
+        want[0] -= extra
+        owner = np.zeros(len(grid), np.int32)
+
+        def cut(idx, r0, r1):
+            if r1 - r0 == 1 or len(idx) == 0:
+                owner[idx] = r0
+                return
+            m = (r0 + r1) // 2
+            x, y = grid[idx, 0], grid[idx, 1]
+            vertical = (x.max() - x.min()) >= (y.max() - y.min())
+            o = idx[np.lexsort((y, x) if vertical else (x, y))]
+            cum = np.cumsum(costs[o].astype(np.float64))
+            frac = want[r0:m].sum() / max(1e-30, want[r0:r1].sum())
+            k = int(np.searchsorted(cum, frac * cum[-1], side="left"))
+            if k < len(cum) and (k == 0 or abs(cum[k] - frac * cum[-1]) < abs(cum[k - 1] - frac * cum[-1])):
+                k += 1  # the nearer of the tile boundaries around the target
+            cut(o[:k], r0, m)
+            cut(o[k:], m, r1)
+
+        cut(np.arange(len(grid)), 0, world)
+        return cls(width, height, world, side, owner, costs if heavy_first else None)
+
     def pixel_map(self, rank: int) -> np.ndarray:
         return E.packed_pixel_map(self.tiles[rank], self.width, self.height)
 

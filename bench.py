@@ -329,8 +329,9 @@ def main():
                     help="frames per launch (atr_render_start_cameras, at most MAX_FRAME_CAMS = 24); 1 = one frame per launch; "
                          "0 = the K steps in as few launches per stream as the cap allows, at least 4 x ranks "
                          "(a launch boundary inside a stream and the last launch's tail are the overheads)")
-    ap.add_argument("--plan", default="cost", choices=["cost", "rr"],
-                    help="N>1 tile deal: measured-cost longest-first (default) or round-robin")
+    ap.add_argument("--plan", default="cost", choices=["cost", "curve", "rr"],
+                    help="N>1 tile deal: measured-cost longest-first (default), equal-cost runs of the "
+                         "near-rectangles (compact shards), or round-robin")
     ap.add_argument("--calib-frames", type=int, default=3,
                     help="cost plan: per-tile costs summed over this many of the run's frames (one calibration render each)")
     ap.add_argument("--cell-split", default="",
@@ -403,6 +404,7 @@ def selftest(args):
     n = len(S.E.shard_grid(W, H, side))
     costs = (np.arange(n) * 7919) % 97 + 1  # deterministic stand-in for the calibration render
     plan = S.ShardPlan.balanced(costs, W, H, world, side, max(0.0, args.rank0_extra)) if args.plan == "cost" \
+        else S.ShardPlan.curve(costs, W, H, world, side, max(0.0, args.rank0_extra)) if args.plan == "curve" \
         else S.ShardPlan(W, H, world, side)
     F = args.frames_per_launch
     pix = torch.from_numpy(plan.pixel_map(rank).astype(np.int64)) if plan.sizes[rank] else torch.zeros(0, dtype=torch.int64)
@@ -568,7 +570,7 @@ def run(args):
     sim = world == 1 and args.sim_world > 1
     pw, pr = (args.sim_world, args.sim_rank) if sim else (world, rank)  # the plan's world and rank
     heavy_first = args.tile_order == "cost"
-    if (pw > 1 and args.plan == "cost") or (pw == 1 and args.single_tiles == "cost"):
+    if (pw > 1 and args.plan in ("cost", "curve")) or (pw == 1 and args.single_tiles == "cost"):
         # measured on frames BEFORE the timed window (the warmup's orbit positions, or the positions
         # just before them): a live renderer only has its previous frames
         ks = calib_frames(args)
@@ -587,7 +589,8 @@ def run(args):
                                                         dev if backend == "nccl" else "cpu")[0]) / 1e6
         if world > 1:
             costs = S.shared_costs(costs, rank, dist, dev if backend == "nccl" else "cpu")
-        plan = S.ShardPlan.balanced(costs, W, H, pw, args.side, args.rank0_extra, heavy_first)
+        mk = S.ShardPlan.curve if (pw > 1 and args.plan == "curve") else S.ShardPlan.balanced
+        plan = mk(costs, W, H, pw, args.side, args.rank0_extra, heavy_first)
     else:
         plan = S.ShardPlan(W, H, pw, args.side)
     sizes = plan.sizes
@@ -997,7 +1000,7 @@ def run(args):
                "total_ray_casts_per_frame": round(casts_total / max(1, casts_frames))}
         if steady:
             out["steady_state"] = steady
-        if (pw > 1 and args.plan == "cost") or args.cell_split or args.cell_order != "list" or \
+        if (pw > 1 and args.plan in ("cost", "curve")) or args.cell_split or args.cell_order != "list" or \
             (pw == 1 and args.single_tiles == "cost"):
             out["config"]["calibration_frames"] = calib_frames(args)  # orbit positions, all before the timed ones
         if check is not None:

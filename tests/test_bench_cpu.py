@@ -20,13 +20,15 @@ def _json_line(out):
     return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("n,exchange", [(2, "bgr"), (2, "bgrx"), (3, "bgr"), (8, "bgr"), (2, "masked"), (3, "masked"), (8, "masked")])
-def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n, exchange):
+@pytest.mark.parametrize("n,exchange,plan", [(2, "bgr", "cost"), (2, "bgrx", "cost"), (3, "bgr", "cost"), (8, "bgr", "cost"),
+                                            (2, "masked", "cost"), (3, "masked", "cost"), (8, "masked", "cost"),
+                                            (3, "masked", "curve")])
+def test_bench_gpus_n_spawns_n_ranks_and_assembles_frames(n, exchange, plan):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--selftest",
-                        "--steps", "11", "--warmup", "1", "--frames-per-launch", "4", "--exchange", exchange],
+                        "--steps", "11", "--warmup", "1", "--frames-per-launch", "4", "--exchange", exchange, "--plan", plan],
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _json_line(r.stdout)
@@ -55,6 +57,31 @@ def test_launch_sizes_are_balanced(k, f, streams):
     if k >= streams:  # round-robin: every stream gets the same frames, to one
         per = [sum(s[q::streams]) for q in range(streams)]
         assert max(per) - min(per) <= 1
+
+
+def test_curve_plan_is_compact_and_balanced():
+    """ShardPlan.curve: every grid tile owned once, the recursive bisection balanced within about a
+    tile's cost per cut (rank 0 lighter by its assembly share), and each rank's tiles compact (a
+    near-rectangle: its bounding box at most twice its tiles' area)."""
+    import numpy as np
+    from atray_amd import shard as S
+    W, H, side = 1920, 1080, 32
+    grid = S.E.shard_grid(W, H, side)
+    costs = (np.arange(len(grid)) * 7919) % 97 + 1
+    for world in (2, 4, 8):
+        p = S.ShardPlan.curve(costs, W, H, world, side, 0.1)
+        assert sorted(np.concatenate([np.asarray(t).reshape(-1, 4)[:, 0] + W * np.asarray(t).reshape(-1, 4)[:, 1]
+                                      for t in p.tiles])) == sorted(grid[:, 0] + W * grid[:, 1])
+        loads = np.array([costs[p.owner == r].sum() for r in range(world)], np.float64)
+        extra = 0.1 * costs.sum() / world
+        share = (costs.sum() + extra) / world
+        assert abs(loads[0] - (share - extra)) <= 3 * costs.max()
+        assert np.all(np.abs(loads[1:] - share) <= 3 * costs.max())
+        for t in p.tiles:
+            t = np.asarray(t).reshape(-1, 4)
+            area = (t[:, 2].max() - t[:, 0].min() + 1) * (t[:, 3].max() - t[:, 1].min() + 1)
+            own = ((t[:, 2] - t[:, 0] + 1) * (t[:, 3] - t[:, 1] + 1)).sum()
+            assert area <= 2 * own, (world, area, own)
 
 
 def test_orbit_cameras_are_distinct():

@@ -94,6 +94,44 @@ def test_path_workspaces_bounded_over_many_streams(eng):
         assert torch.equal(fb, want[0]) and torch.equal(casts, want[1])
 
 
+def test_path_workspace_grows_once_to_a_whole_batch():
+    """A workspace holds its first launch's paths rounded up to 2^24 (within one batch); a later
+    launch that needs more grows it straight to a whole batch, so launches after that never regrow
+    (round 6: a regrow inside a timed multi-frame run cost a c4 line 4x). 2^26-path batches;
+    128x128 at 64 spp, 1 bounce (no queue sort: 144 B per path): 1, 17 and 24 frames per launch, and
+    every frame of the 24-frame launch equals the one-frame render."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    W, H = 128, 128
+    cam = E.camera(W, H, 64, 1)
+    e = make_engine()
+    try:
+        e.set_tuning(path_batch_log2=26)
+        want = render(e, cam, E.ATR_KERNEL_PATHS)  # 1.05 M paths
+        b1 = e.workspace_info()["device_bytes"]
+        assert (1 << 24) * 144 <= b1 < (1 << 24) * 144 + (1 << 20), b1
+        sizes = []
+        for n in (17, 24, 17):  # 17.8 M paths: past 2^24 -> one 2^26 batch; then no change
+            fb = torch.zeros(n * W * H, dtype=torch.int32, device="cuda")
+            casts = torch.zeros(n * W * H, dtype=torch.int32, device="cuda")
+            fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb.data_ptr(), None, None, None, casts.data_ptr(), None)
+            e.render_start_cameras([cam] * n, [[0, 0, W - 1, H - 1]], fr, W * H, SEED,
+                                   variant=E.ATR_KERNEL_PATHS)
+            assert e.wait()[0] == 0
+            torch.cuda.synchronize()
+            info = e.workspace_info()
+            assert info["workspaces"] == 1, info
+            sizes.append(info["device_bytes"])
+            for f in (0, n - 1):
+                assert torch.equal(fb[f * W * H:(f + 1) * W * H], want[0])
+                assert torch.equal(casts[f * W * H:(f + 1) * W * H], want[1])
+        assert (1 << 26) * 144 <= sizes[0] < (1 << 26) * 144 + (1 << 20), sizes
+        assert sizes[1] == sizes[0] == sizes[2], sizes
+    finally:
+        e.close()
+        torch.cuda.empty_cache()
+
+
 def test_path_workspace_out_of_memory_halves_the_batch():
     """With most of the device memory taken (a torch allocation of all but ~600 MB), a PATHS render
     whose default batch needs a 1.2-GB workspace (480x270 at 64 spp: 2^23 paths) halves its batch
