@@ -82,14 +82,16 @@ struct BlockSet {
     DevBuf dev_tile;  // owning tile per packed slot (atr_packed_tile_ray_casts; built on first use)
     bool tile_ready = false;
     int64_t packed_pixels = 0;
-    // one event per stream that launched work reading this set, recorded after its latest such
-    // launch: before the set's buffers are rewritten or freed, every one of them is waited for
-    std::vector<std::pair<hipStream_t, hipEvent_t>> evs;
-    // single-frame plan (plan.hip): per-base-block clocks of the last single-frame launch, the
-    // planned block list built from them on the GPU, the stream that owns the pair
+    // single-frame plan (plan.hip), double-buffered: launch n (parity n & 1) renders from the list
+    // planned on the costs of launch n - 2 and writes its per-base-block clocks into its parity's
+    // cost half; the plan kernels then run on the context's plan stream, after the render and
+    // beside launch n + 1, and rebuild that parity's list from them (plan_ev[parity] after them)
     DevBuf cost, cost_last, plan_work, plan_blocks;
     int32_t max_split = 0;
-    bool plan_ready = false;
+    bool plan_ready = false;   // a plan was issued on this set (the buffers hold plan state)
+    bool plan_valid[2] = {};   // a list is built (or being built) in that parity's half
+    hipEvent_t plan_ev[2] = {};
+    int plan_par = 0;          // the parity of the next planned launch
     hipStream_t plan_stream = nullptr;
 };
 
@@ -223,7 +225,9 @@ struct atr_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t last_stream = nullptr;
-    hipEvent_t ev_start = nullptr, ev_stop = nullptr, ev_done = nullptr;
+    // ev_start before every render; its completion event ev_last: the traced-ray set's event of
+    // launch_render (one record per launch), or ev_stop for a launch without traced rays
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr, ev_last = nullptr;
     bool have_render = false;
     int32_t last_ntiles = 0;
     std::vector<DevBuf> scene_bufs;
@@ -277,6 +281,7 @@ struct atr_ctx {
     // regrowth and progressive group buffers wait for all of them)
     std::vector<std::pair<hipStream_t, hipEvent_t>> stream_ev;
     int32_t wave_slots = 0;  // CUs x 4 SIMDs x 6 waves (single-frame plan policy), 0 until first use
+    hipStream_t plan_side = nullptr;  // the single-frame plan kernels' stream (created on first use)
 };
 
 namespace {
@@ -332,15 +337,23 @@ hipError_t wait_list(const std::vector<std::pair<hipStream_t, hipEvent_t>>& list
     return hipSuccess;
 }
 
-// Record that a launch on stream s is in flight (and reads block set bs, if any).
-hipError_t note_launch(atr_ctx* c, hipStream_t s, BlockSet* bs) {
-    hipError_t e;
-    if (bs && (e = note_stream(bs->evs, s)) != hipSuccess) return e;
-    return note_stream(c->stream_ev, s);
+// Record that a launch on stream s is in flight. (A block set's buffers are rewritten or freed
+// only after every stream's latest launch, wait_all: a cache miss or a first per-tile query, rare,
+// so launches record no event per block set.) A render whose completion event is one of the
+// traced-ray ring's (ring = true) records nothing here: wait_all also waits for every ring event in
+// use, and a ring event is re-recorded only on a stream that first waited for its previous record
+// (launch_render), so it still covers every launch that recorded it.
+hipError_t note_launch(atr_ctx* c, hipStream_t s, bool ring = false) {
+    return ring ? hipSuccess : note_stream(c->stream_ev, s);
 }
 
 // Wait for every launch of this context still in flight, on any stream.
-hipError_t wait_all(atr_ctx* c) { return wait_list(c->stream_ev); }
+hipError_t wait_all(atr_ctx* c) {
+    hipError_t e = wait_list(c->stream_ev);
+    for (int k = 0; e == hipSuccess && k < kQueueSlots; ++k)
+        if (c->tused[k]) e = hipEventSynchronize(c->tev[k]);
+    return e;
+}
 
 void free_scene(atr_ctx* c) {
     for (DevBuf& b : c->scene_bufs) (void)hipFree(b.p);
@@ -365,7 +378,7 @@ BlockSet* get_blocks(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t 
     c->block_use[lru] = ++c->use_clock;
     // the slot may still be read by in-flight kernels of earlier renders, on several streams
     {
-        const hipError_t e = wait_list(b.evs);
+        const hipError_t e = wait_all(c);
         if (e != hipSuccess) { rc = -(1000 + int(e)); return nullptr; }
     }
     b.tiles.assign(tiles, tiles + ntiles);
@@ -439,19 +452,32 @@ int auto_sched(int32_t variant, const atr_camera& cam) {
 // this stream (the base list the first time), adds each cell's clocks into the set's cost buffer,
 // and the plan kernels then build the next list from them. Another stream, a user cell plan for the
 // size or frame_plan 0 -> the plain base-list launch.
-// The render's completion events (ev_stop, ev_done) are recorded between the render and the plan
-// kernels, so atr_render_wait and atr_last_kernel_ms see the render alone.
-hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s);
+// The render's completion event (ev_last) is recorded right after the render; the plan kernels
+// run on the plan stream, so atr_render_wait, atr_last_kernel_ms and the next launch on s do not
+// wait for them.
+hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s, hipEvent_t* done = nullptr);
+
+// One completion record per launch: `done` (the traced-ray set's event launch_render recorded after
+// the render) when there is one, else ev_stop.
+hipError_t record_stop(atr_ctx* c, hipStream_t s, hipEvent_t done) {
+    if (done) {
+        c->ev_last = done;
+        return hipSuccess;
+    }
+    c->ev_last = c->ev_stop;
+    return hipEventRecord(c->ev_stop, s);
+}
+
 int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStream_t s) {
     const int32_t nb = int32_t(bs->host.size());
     // on top of a user cell plan too: its classes order the base list (and the multi-frame
     // launches), the frame plan re-orders that list for single frames by their measured cost
     const bool use = c->tune.frame_plan && nb > 0 && sched != kSchedPaths &&
                      (!bs->plan_ready || bs->plan_stream == s);
+    hipEvent_t done = nullptr;
     if (!use) {
-        HIPCHK(launch_render(c, P, sched, s));
-        HIPCHK(hipEventRecord(c->ev_stop, s));
-        HIPCHK(hipEventRecord(c->ev_done, s));
+        HIPCHK(launch_render(c, P, sched, s, &done));
+        HIPCHK(record_stop(c, s, done));
         return ATR_OK;
     }
     // A launch whose cells fit the chip's wave slots at once (a shard's frame: 4,050 cells of an
@@ -467,30 +493,46 @@ int launch_planned(atr_ctx* c, BlockSet* bs, RenderParams& P, int sched, hipStre
     const bool small = nb <= c->wave_slots;
     const float split2 = small ? 0.10f : -1.f, split4 = small ? 0.03f : -1.f;
     const int32_t max_split = std::max<int32_t>(1, small ? nb / 5 : nb / 25);  // spare blocks for splits
+    const size_t cap = size_t(nb + max_split);
     int rc;
     const bool fresh = !bs->cost.p;  // the buffers start zeroed; each plan leaves them zeroed
-    if ((rc = ensure_buf(bs->cost, size_t(nb) * sizeof(unsigned long long), true))) return rc;
+    if ((rc = ensure_buf(bs->cost, 2 * size_t(nb) * sizeof(unsigned long long), true))) return rc;
     if ((rc = ensure_buf(bs->cost_last, size_t(nb) * sizeof(unsigned long long), false))) return rc;
     if ((rc = ensure_buf(bs->plan_work, atr_plan_work_bytes(nb), true))) return rc;
-    if ((rc = ensure_buf(bs->plan_blocks, size_t(nb + max_split) * sizeof(DBlock), false))) return rc;
+    if ((rc = ensure_buf(bs->plan_blocks, 2 * cap * sizeof(DBlock), false))) return rc;
+    if (!c->plan_side) HIPCHK(hipStreamCreateWithFlags(&c->plan_side, hipStreamNonBlocking));
+    for (hipEvent_t& e : bs->plan_ev)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!bs->plan_ready && !fresh) {  // a rebuilt set reuses buffers a plan may not have cleared
-        HIPCHK(hipMemsetAsync(bs->cost.p, 0, size_t(nb) * sizeof(unsigned long long), s));
+        HIPCHK(hipMemsetAsync(bs->cost.p, 0, 2 * size_t(nb) * sizeof(unsigned long long), s));
         // and the work area's thresholds (learned on the old list, whose nb and max_split differ):
         // back to the documented zeroed state (class 0, no split) for the first plan on this list
         HIPCHK(hipMemsetAsync(bs->plan_work.p, 0, atr_plan_work_bytes(nb), s));
     }
-    bs->max_split = max_split;
-    if (bs->plan_ready) {
-        P.blocks = static_cast<const DBlock*>(bs->plan_blocks.p);
-        P.nblocks = nb + max_split;
+    if (!bs->plan_ready) {
+        bs->plan_valid[0] = bs->plan_valid[1] = false;
+        bs->plan_par = 0;
     }
-    P.block_cost = static_cast<unsigned long long*>(bs->cost.p);
-    HIPCHK(launch_render(c, P, sched, s));
-    HIPCHK(hipEventRecord(c->ev_stop, s));
-    HIPCHK(hipEventRecord(c->ev_done, s));
-    HIPCHK(atr_launch_plan(static_cast<const DBlock*>(bs->dev.p), nb, static_cast<unsigned long long*>(bs->cost.p),
-                           static_cast<unsigned long long*>(bs->cost_last.p), bs->plan_work.p,
-                           static_cast<DBlock*>(bs->plan_blocks.p), max_split, split2, split4, s));
+    bs->max_split = max_split;
+    const int par = bs->plan_par;
+    DBlock* list = static_cast<DBlock*>(bs->plan_blocks.p) + size_t(par) * cap;
+    unsigned long long* cost = static_cast<unsigned long long*>(bs->cost.p) + size_t(par) * size_t(nb);
+    if (bs->plan_valid[par]) {  // this parity's list, built beside the previous launch, and its cost
+        HIPCHK(hipStreamWaitEvent(s, bs->plan_ev[par], 0));  // half cleared by the same kernels
+        P.blocks = list;
+        P.nblocks = int32_t(cap);
+    }
+    P.block_cost = cost;
+    HIPCHK(launch_render(c, P, sched, s, &done));
+    HIPCHK(record_stop(c, s, done));
+    HIPCHK(hipStreamWaitEvent(c->plan_side, c->ev_last, 0));
+    HIPCHK(atr_launch_plan(static_cast<const DBlock*>(bs->dev.p), nb, cost,
+                           static_cast<unsigned long long*>(bs->cost_last.p), bs->plan_work.p, list, max_split,
+                           split2, split4, c->plan_side));
+    HIPCHK(hipEventRecord(bs->plan_ev[par], c->plan_side));
+    HIPCHK(note_stream(c->stream_ev, c->plan_side));
+    bs->plan_valid[par] = true;
+    bs->plan_par = par ^ 1;
     bs->plan_ready = true;
     bs->plan_stream = s;
     return ATR_OK;
@@ -745,7 +787,8 @@ hipError_t launch_kernels(atr_ctx* c, RenderParams& P, int sched, hipStream_t s)
 
 // Launch a render schedule; the traced rays go into a zeroed set of 64 spread counters from the
 // ring, then one add to the caller's accumulator.
-hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) {
+hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s, hipEvent_t* done) {
+    if (done) *done = nullptr;
     if (!P.traced_rays) return launch_kernels(c, P, sched, s);
     const int k = c->tnext;
     c->tnext = (k + 1) % kQueueSlots;
@@ -759,6 +802,7 @@ hipError_t launch_render(atr_ctx* c, RenderParams& P, int sched, hipStream_t s) 
     if (e != hipSuccess) return e;
     if ((e = hipEventRecord(c->tev[k], s)) != hipSuccess) return e;
     c->tused[k] = true;
+    if (done) *done = c->tev[k];
     return hipSuccess;
 }
 
@@ -1017,13 +1061,12 @@ int atr_create(int device, atr_ctx** out) {
         HIPCHK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&c->ev_start));
         HIPCHK(hipEventCreate(&c->ev_stop));
-        HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
         HIPCHK(hipMalloc(&c->d_error, 16));
         HIPCHK(hipMemset(c->d_error, 0, 16));
         HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
         HIPCHK(hipMalloc(&c->tring, kQueueSlots * kTraceBytes));
         HIPCHK(hipMemset(c->tring, 0, kQueueSlots * kTraceBytes));
-        for (hipEvent_t& e : c->tev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t& e : c->tev) HIPCHK(hipEventCreate(&e));  // timed: a launch's ev_last
         return ATR_OK;
     }();
     if (rc != ATR_OK) {
@@ -1072,7 +1115,8 @@ int atr_destroy(atr_ctx* c) {
         if (b.dev_tile.p) (void)hipFree(b.dev_tile.p);
         for (DevBuf* d : {&b.cost, &b.cost_last, &b.plan_work, &b.plan_blocks})
             if (d->p) (void)hipFree(d->p);
-        for (auto& se : b.evs) (void)hipEventDestroy(se.second);
+        for (hipEvent_t e : b.plan_ev)
+            if (e) (void)hipEventDestroy(e);
     }
     for (auto& se : c->stream_ev) (void)hipEventDestroy(se.second);
     for (auto& w : c->path_ws) {
@@ -1089,8 +1133,8 @@ int atr_destroy(atr_ctx* c) {
     if (c->tring) (void)hipFree(c->tring);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
-    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->plan_side) (void)hipStreamDestroy(c->plan_side);
     for (int i = 0; i < 2; ++i) {
         if (c->split_stream[i]) (void)hipStreamDestroy(c->split_stream[i]);
         if (c->split_join[i]) (void)hipEventDestroy(c->split_join[i]);
@@ -1340,7 +1384,7 @@ int atr_render_start_ex(atr_ctx* c, const atr_camera* cam, const atr_tile* tiles
     apply_tuning(c, P);
     HIPCHK(hipEventRecord(c->ev_start, s));
     if ((rc = launch_planned(c, bs, P, wave, s))) return rc;
-    HIPCHK(note_launch(c, s, bs));
+    HIPCHK(note_launch(c, s, c->ev_last != c->ev_stop));  // a ring event covers it
     c->have_render = true;
     c->last_stream = s;
     c->last_ntiles = ntiles;
@@ -1394,12 +1438,10 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
     P.error_flag = c->d_error;
     apply_tuning(c, P);
     HIPCHK(hipEventRecord(c->ev_start, s));
-    bool recorded = false;
     if (nframes == 1) {  // one frame: the single-frame plan applies
         P.nblocks = nb;
         P.frame_stride = frame_stride;
         if ((rc = launch_planned(c, bs, P, sched, s))) return rc;
-        recorded = true;
     } else {  // one launch over frames x blocks (render_kernel / paths: fidx)
         P.nblocks = nb * nframes;
         P.frame_blocks = nb;
@@ -1409,13 +1451,11 @@ int start_frames(atr_ctx* c, const atr_camera* cams, int32_t ncams, const atr_ti
             P.nfcam = ncams;
             for (int32_t f = 0; f < ncams; ++f) P.fcam[f] = cams[f];
         }
-        HIPCHK(launch_render(c, P, sched, s));
+        hipEvent_t done = nullptr;
+        HIPCHK(launch_render(c, P, sched, s, &done));
+        HIPCHK(record_stop(c, s, done));
     }
-    if (!recorded) {
-        HIPCHK(hipEventRecord(c->ev_stop, s));
-        HIPCHK(hipEventRecord(c->ev_done, s));
-    }
-    HIPCHK(note_launch(c, s, bs));
+    HIPCHK(note_launch(c, s, c->ev_last != c->ev_stop));  // a ring event covers it
     c->have_render = true;
     c->last_stream = s;
     c->last_ntiles = ntiles;
@@ -1663,9 +1703,8 @@ int atr_render_start_progressive(atr_ctx* c, const atr_camera* cam, const atr_ti
         HIPCHK(hipEventRecord(c->prog_ev[size_t(g)], s));
         c->prog_end[size_t(g)] = e;
     }
-    HIPCHK(hipEventRecord(c->ev_stop, s));
-    HIPCHK(hipEventRecord(c->ev_done, s));
-    HIPCHK(note_launch(c, s, nullptr));
+    HIPCHK(record_stop(c, s, nullptr));
+    HIPCHK(note_launch(c, s));
     c->have_render = true;
     c->prog_active = true;
     c->last_stream = s;
@@ -1685,7 +1724,7 @@ int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
     HIPCHK(hipSetDevice(c->device));
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
-        const hipError_t q = hipEventQuery(c->ev_done);
+        const hipError_t q = hipEventQuery(c->ev_last);
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) return -(1000 + int(q));
         const auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
@@ -1697,10 +1736,10 @@ int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
                     if (qg != hipSuccess) break;
                     *tiles_done = c->prog_end[g];
                 }
-                // every group finished since ev_done was queried: the render is done (ev_done
+                // every group finished since ev_last was queried: the render is done (ev_last
                 // follows the last group on the same stream), report it as done, not running
                 if (g == c->prog_end.size() && !c->prog_end.empty()) {
-                    HIPCHK(hipEventSynchronize(c->ev_done));
+                    HIPCHK(hipEventSynchronize(c->ev_last));
                     break;
                 }
             }
@@ -1721,8 +1760,8 @@ int atr_render_wait(atr_ctx* c, uint32_t timeout_ms, int32_t* tiles_done) {
 
 int atr_last_kernel_ms(atr_ctx* c, float* ms) {
     if (!c || !ms || !c->have_render) return ATR_E_INVALID;
-    HIPCHK(hipEventSynchronize(c->ev_stop));
-    HIPCHK(hipEventElapsedTime(ms, c->ev_start, c->ev_stop));
+    HIPCHK(hipEventSynchronize(c->ev_last));
+    HIPCHK(hipEventElapsedTime(ms, c->ev_start, c->ev_last));
     return ATR_OK;
 }
 
@@ -1737,7 +1776,7 @@ int atr_unpack(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t width,
     if (!bs) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
     HIPCHK(atr_launch_unpack(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed, image, s));
-    HIPCHK(note_launch(c, s, bs));
+    HIPCHK(note_launch(c, s));
     return ATR_OK;
 }
 
@@ -1788,7 +1827,7 @@ int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles,
                     st[k++] = owner[size_t(blk.y0 + (lane >> 3)) * size_t(width) + size_t(blk.x0 + (lane & 7))];
         }
         // a hipMemcpy below may overwrite a buffer a kernel on another stream still reads
-        HIPCHK(wait_list(bs->evs));
+        HIPCHK(wait_all(c));
         const size_t need = st.size() * sizeof(int32_t);
         if (bs->dev_tile.n < need) {
             if (bs->dev_tile.p) (void)hipFree(bs->dev_tile.p);
@@ -1802,7 +1841,7 @@ int atr_packed_tile_ray_casts(atr_ctx* c, const atr_tile* tiles, int32_t ntiles,
     HIPCHK(hipMemsetAsync(out, 0, sizeof(int64_t) * size_t(nframes) * size_t(ntiles), s));
     HIPCHK(atr_launch_packed_tile_casts(static_cast<const int32_t*>(bs->dev_tile.p), n, casts, frame_stride, nframes,
                                         ntiles, reinterpret_cast<unsigned long long*>(out), s));
-    HIPCHK(note_launch(c, s, bs));
+    HIPCHK(note_launch(c, s));
     return ATR_OK;
 }
 
@@ -1863,7 +1902,7 @@ int atr_unpack_masked(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t
     HIPCHK(atr_launch_unpack_masked(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed,
                                     nframes, own, image, image_stride, static_cast<uint32_t*>(goff), s));
     HIPCHK(hipFreeAsync(goff, s));
-    HIPCHK(note_launch(c, s, bs));
+    HIPCHK(note_launch(c, s));
     return ATR_OK;
 }
 
@@ -1877,7 +1916,7 @@ int atr_render_plan_info(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int3
     if (!bs) return rc;
     *nplanned = 0;
     if (!bs->plan_ready) return ATR_OK;
-    HIPCHK(wait_list(bs->evs));
+    HIPCHK(wait_all(c));  // the plan stream's kernels too
     const int64_t nb = int64_t(bs->host.size()), np = nb + bs->max_split;
     *nplanned = np;
     if (cap < np) return ATR_OK;  // size query

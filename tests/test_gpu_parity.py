@@ -370,7 +370,7 @@ def test_frame_plan_changes_no_output(eng, variant):
             want = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
                                                          variant=variant)]
             eng.set_tuning(frame_plan=1)
-            for _ in range(3):  # the first launch measures, the later ones dispatch by the plan
+            for _ in range(5):  # the first two measure, the later ones dispatch by a plan (one per parity)
                 got = [run(eng, cam, variant=variant), run(eng, cam, tiles=tiles, layout=E.ATR_LAYOUT_PACKED,
                                                             variant=variant)]
                 for a, b in zip(want, got):
@@ -388,6 +388,41 @@ def test_frame_plan_changes_no_output(eng, variant):
             got = run(eng, cam, variant=variant)
             for k in ("fb", "face", "t", "casts"):
                 assert np.array_equal(np.asarray(want[k]).view(np.uint32), np.asarray(got[k]).view(np.uint32)), k
+    finally:
+        eng.set_tuning(**base)
+
+
+@pytest.mark.parametrize("variant", [E.ATR_KERNEL_AUTO, E.ATR_KERNEL_FLAT])
+def test_frame_plan_back_to_back_launches(eng, variant):
+    """Single-frame launches issued back to back with no wait between them (the live view's
+    pattern, several in flight): the plan kernels run on the context's plan stream beside the next
+    launch, double-buffered (launch n renders from the plan of launch n - 2's costs, capi.cpp
+    launch_planned), so each launch must wait for exactly the plan and cleared cost half it uses.
+    Eight launches over two alternating cameras, every output equal to the plain list order's."""
+    upload(eng, "Dragon", True)
+    W, H = 480, 270
+    cams = [E.camera(W, H, 1, 1), E.camera(W, H, 1, 1, eye=(0.3, 2.0, 0.6))]
+    base = eng.tuning()
+    try:
+        eng.set_tuning(frame_plan=0)
+        want = [run(eng, c, variant=variant) for c in cams]
+        eng.set_tuning(frame_plan=1)
+        n = W * H
+        fb = torch.zeros(8, n, dtype=torch.int32, device="cuda")
+        casts = torch.zeros(8, n, dtype=torch.int32, device="cuda")
+        traced = torch.zeros(8, dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        for i in range(8):
+            fr = E.atr_frame(E.ATR_LAYOUT_IMAGE, fb[i].data_ptr(), None, None, None, casts[i].data_ptr(),
+                             traced[i:i + 1].data_ptr())
+            eng.render_start(cams[i % 2], [[0, 0, W - 1, H - 1]], fr, SEED, stream=s, variant=variant)
+        assert eng.wait()[0] == 0
+        torch.cuda.synchronize()
+        for i in range(8):
+            w = want[i % 2]
+            assert np.array_equal(fb[i].cpu().numpy().view(np.uint32), w["fb"].ravel()), i
+            assert np.array_equal(casts[i].cpu().numpy().view(np.uint32), w["casts"].ravel()), i
+            assert int(traced[i].item()) == w["traced"], i
     finally:
         eng.set_tuning(**base)
 

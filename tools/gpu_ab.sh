@@ -18,7 +18,7 @@ tail -1 $O/pytest.log
 fi
 run() {  # name, timeout, lib, args
   ATRAY_LIB=$3 timeout -k 10 $2 python3 bench.py --no-pmc --no-cpu-baseline --no-prep --no-steady "${@:4}" > $O/$1.json 2> $O/$1.err || { tail -5 $O/$1.err; exit 1; }
-  python3 -c "import json; d=json.loads(open('$O/$1.json').read().strip().splitlines()[-1]); print('$1', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'])"
+  python3 -c "import json; d=json.loads(open('$O/$1.json').read().strip().splitlines()[-1]); print('$1', d['value'], d['ms_per_step'], d['single_frame']['latency_ms'], d['single_frame']['kernel_ms'], d['single_frame']['mrays_s'])"
 }
 for i in 1 2; do
   n=0
