@@ -1921,7 +1921,9 @@ int atr_render_plan_info(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int3
     *nplanned = np;
     if (cap < np) return ATR_OK;  // size query
     std::vector<DBlock> h(static_cast<size_t>(np));
-    HIPCHK(hipMemcpy(h.data(), bs->plan_blocks.p, size_t(np) * sizeof(DBlock), hipMemcpyDeviceToHost));
+    // the list built last (from the last planned launch's costs, in that launch's parity half)
+    const DBlock* last = static_cast<const DBlock*>(bs->plan_blocks.p) + size_t(bs->plan_par ^ 1) * size_t(np);
+    HIPCHK(hipMemcpy(h.data(), last, size_t(np) * sizeof(DBlock), hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < np; ++i) {
         if (base_out) base_out[i] = h[size_t(i)].base;
         if (mask_hi_lo_out) {

@@ -173,10 +173,11 @@ typedef struct {
                                a workspace too small for a later launch grows to a whole batch.
                                2^29 measured 5-7x slower */
     int32_t cluster_size;   /* primitives per leaf cluster, 1..16; default 16 */
-    int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous one
-                               dispatches its tiles' cells by that launch's measured cost, heaviest
-                               first, the heaviest 1 % over two waves (built on the GPU after each
-                               such launch); 0: list order; default 1. With an
+    int32_t frame_plan;     /* 1: a single-frame launch on the stream of the previous ones
+                               dispatches its tiles' cells by the measured cost of the launch two
+                               before it, heaviest first, the heaviest 1 % over two waves (built on
+                               the GPU on the context's plan stream after each such launch, beside
+                               the next one); 0: list order; default 1. With an
                                atr_set_cell_plan plan for the image size it re-orders that plan's
                                block list */
     int32_t path_camera_occ; /* PATHS: waves/SIMD of the camera-ray and bounce launches, 5..7, */
@@ -352,7 +353,8 @@ int atr_unpack_masked(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32
 #define ATR_PLAN_CLASS(c) ((uint8_t)(((c) & 7) << 4))
 enum { ATR_PLAN_PRIO = 0x80 };
 int atr_set_cell_plan(atr_ctx* ctx, int32_t width, int32_t height, const uint8_t* plan);
-/* Diagnostic, synchronous: the single-frame plan of a tile list (tuning frame_plan): *nplanned =
+/* Diagnostic, synchronous: the single-frame plan of a tile list (tuning frame_plan) built last,
+   from the last planned launch's costs (the list the launch after next dispatches by): *nplanned =
    the planned block list's length (0 = no plan yet; a size query when cap is too small); per
    planned block its base block index (base_out) and lane mask (2 u32, lo then hi); cost_out = the
    clocks per base block of the last measured launch (the base list's length). */
