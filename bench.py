@@ -767,8 +767,16 @@ def run(args):
             launch_ev.append((nf, ev_a, ev))
         if pw > 1:
             with torch.cuda.stream(streams[q]):
+                # the exchange's encoding first (it heads the critical path: encode, sizes, streams,
+                # rank 0's decode), then the per-tile counters, which only the reduction needs
+                if bgr and own:  # the rank's frames in 3 bytes per pixel (part of its per-rank work)
+                    eng.pack_bgr(fbs[q].data_ptr(), nf * own, send3[q].data_ptr(), stream=streams[q].cuda_stream)
+                if masked and own and pr != 0:  # the rank's frames as one masked stream (rank 0 keeps its own)
+                    eng.pack_bgr_masked(fbs[q].data_ptr(), nf * own, bgv[0], enc[q].data_ptr(), nbytes[q].data_ptr(),
+                                        stream=streams[q].cuda_stream)
                 ts = tsum[q]
-                ts.zero_()
+                if rank == 0 and not sim:  # the reduction lands in rank 0's buffer: clear it; other
+                    ts.zero_()             # ranks' stay zero outside their own tile columns
                 if own:  # the reference's per-tile counters of this rank's tiles, scattered into the grid
                     eng.packed_tile_ray_casts(tiles, W, H, casts[q].data_ptr(), nf, own, tcasts[q].data_ptr(),
                                               stream=streams[q].cuda_stream)
@@ -777,11 +785,6 @@ def run(args):
                         ts.index_copy_(1, tids.cpu(), part.cpu())
                     else:
                         ts.index_copy_(1, tids, part)
-                if bgr and own:  # the rank's frames in 3 bytes per pixel (part of its per-rank work)
-                    eng.pack_bgr(fbs[q].data_ptr(), nf * own, send3[q].data_ptr(), stream=streams[q].cuda_stream)
-                if masked and own and pr != 0:  # the rank's frames as one masked stream (rank 0 keeps its own)
-                    eng.pack_bgr_masked(fbs[q].data_ptr(), nf * own, bgv[0], enc[q].data_ptr(), nbytes[q].data_ptr(),
-                                        stream=streams[q].cuda_stream)
                 launch_nf[j] = nf
                 if sim:
                     pending[j] = (q, [])
