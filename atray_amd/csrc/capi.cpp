@@ -47,6 +47,12 @@ extern "C" size_t atr_plan_work_bytes(int32_t nb);
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s);
 extern "C" int64_t atr_masked_chunks(int64_t n);
 extern "C" int64_t atr_masked_group_words(int64_t npixels);
+extern "C" int atr_unpack_max_sources();
+extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBlock* const* blocks,
+                                                     const int32_t* nblocks, const int64_t* own,
+                                                     const uint8_t* const* in, int32_t width, int32_t nframes,
+                                                     uint32_t* image, int64_t image_stride, uint32_t* goff,
+                                                     hipStream_t s);
 extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                                const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
                                                int64_t image_stride, uint32_t* goff, hipStream_t s);
@@ -1902,6 +1908,47 @@ int atr_unpack_masked(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t
     HIPCHK(atr_launch_unpack_masked(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed,
                                     nframes, own, image, image_stride, static_cast<uint32_t*>(goff), s));
     HIPCHK(hipFreeAsync(goff, s));
+    HIPCHK(note_launch(c, s));
+    return ATR_OK;
+}
+
+int atr_unpack_masked_ranks(atr_ctx* c, int32_t nsrc, const atr_tile* const* tiles, const int32_t* ntiles,
+                            int32_t width, int32_t height, const uint8_t* const* packed, int32_t nframes,
+                            uint32_t* image, int64_t image_stride, void* stream) {
+    if (!c || nsrc < 0 || (nsrc && (!tiles || !ntiles || !packed)) || !image || width <= 0 || height <= 0 ||
+        nframes < 0 || image_stride < int64_t(width) * height)
+        return ATR_E_INVALID;
+    for (int32_t i = 0; i < nsrc; ++i)
+        if (ntiles[i] < 0 || (ntiles[i] && !tiles[i]) || !packed[i]) return ATR_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    if (nsrc == 0 || nframes == 0) return ATR_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
+    const int32_t kMax = atr_unpack_max_sources();
+    for (int32_t i0 = 0; i0 < nsrc; i0 += kMax) {  // one launch pair per kMax sources
+        const int32_t n = std::min(kMax, nsrc - i0);
+        std::vector<const DBlock*> blocks(size_t(n), nullptr);
+        std::vector<int32_t> nb(size_t(n), 0);
+        std::vector<int64_t> own(size_t(n), 0);
+        int64_t words = 0;
+        for (int32_t k = 0; k < n; ++k) {
+            int rc = ATR_OK;
+            // the renders' cached sets (the most recently used slots: a later lookup here does not
+            // evict an earlier one of this batch)
+            BlockSet* bs = get_blocks(c, tiles[i0 + k], ntiles[i0 + k], width, height, rc);
+            if (!bs) return rc;
+            blocks[size_t(k)] = static_cast<const DBlock*>(bs->dev.p);
+            nb[size_t(k)] = int32_t(bs->host.size());
+            own[size_t(k)] = bs->packed_pixels;
+            if (int64_t(nframes) * own[size_t(k)] >= (int64_t(1) << 32)) return ATR_E_INVALID;
+            words += atr_masked_group_words(int64_t(nframes) * own[size_t(k)]);
+        }
+        if (words == 0) continue;
+        void* goff = nullptr;
+        HIPCHK(hipMallocAsync(&goff, sizeof(uint32_t) * size_t(words), s));
+        HIPCHK(atr_launch_unpack_masked_multi(n, blocks.data(), nb.data(), own.data(), packed + i0, width, nframes,
+                                              image, image_stride, static_cast<uint32_t*>(goff), s));
+        HIPCHK(hipFreeAsync(goff, s));
+    }
     HIPCHK(note_launch(c, s));
     return ATR_OK;
 }

@@ -113,6 +113,7 @@ EXPORTS = [
     "atr_mesh_export", "atr_packed_tile_ray_casts", "atr_set_cell_plan", "atr_render_cell_costs",
     "atr_default_tuning", "atr_set_tuning", "atr_get_tuning", "atr_pack_bgr", "atr_scatter_bgr",
     "atr_pack_bgr_masked_bound", "atr_pack_bgr_masked", "atr_scatter_bgr_masked", "atr_unpack_masked",
+    "atr_unpack_masked_ranks",
     "atr_render_plan_info", "atr_workspace_info",
 ]
 # the diagnostic build's extra symbols (include/atray_diag.h; make -C atray_amd/csrc DIAG=1)
@@ -182,6 +183,7 @@ def lib():
         "atr_pack_bgr_masked": ([vp, vp, i64, u32, vp, vp, vp], C.c_int),
         "atr_scatter_bgr_masked": ([vp, vp, i64, vp, vp, vp], C.c_int),
         "atr_unpack_masked": ([vp, vp, i32, i32, i32, vp, i32, vp, i64, vp], C.c_int),
+        "atr_unpack_masked_ranks": ([vp, i32, vp, vp, i32, i32, vp, i32, vp, i64, vp], C.c_int),
         "atr_render_simd_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
@@ -591,6 +593,19 @@ class Engine:
         check(lib().atr_unpack_masked(self.h, C.cast(arr, C.c_void_p), n, int(width), int(height),
                                       C.c_void_p(packed_ptr), int(nframes), C.c_void_p(image_ptr), int(image_stride),
                                       C.c_void_p(stream) if stream else None), "unpack masked")
+
+    def unpack_masked_ranks(self, tiles_list, width, height, packed_ptrs, nframes, image_ptr, image_stride,
+                            stream=None):
+        """Several masked streams (source i: the PACKED render of tiles_list[i], its stream at
+        packed_ptrs[i]) into the same IMAGE frames in one call (atr_unpack_masked_ranks)."""
+        arrs = [t if isinstance(t, tuple) else tiles_array(t) for t in tiles_list]
+        n = len(arrs)
+        tp = (C.c_void_p * max(1, n))(*[C.cast(a, C.c_void_p) for a, _ in arrs])
+        nt = (C.c_int32 * max(1, n))(*[k for _, k in arrs])
+        pp = (C.c_void_p * max(1, n))(*[int(p) for p in packed_ptrs])
+        check(lib().atr_unpack_masked_ranks(self.h, n, tp, nt, int(width), int(height), pp, int(nframes),
+                                            C.c_void_p(image_ptr), int(image_stride),
+                                            C.c_void_p(stream) if stream else None), "unpack masked ranks")
 
     def plan_info(self, tiles, width, height):
         """The single-frame plan of a tile list (diagnostic): (base index per planned block, masks

@@ -734,10 +734,13 @@ def run(args):
                 if rank == 0:
                     if on_host:
                         recv_dev[q].copy_(recv[q])
-                    for r in range(1, world):  # positions from rank r's tile blocks (atr_unpack_masked)
-                        if sizes[r]:
-                            eng.unpack_masked(rtiles[r], W, H, recv_dev[q][int(roff[r]):].data_ptr(), nf,
-                                              images[q].data_ptr(), npx, stream=streams[q].cuda_stream)
+                    # every other rank's stream in one call, positions from its tile blocks
+                    # (atr_unpack_masked_ranks: one launch pair instead of two launches per rank)
+                    src = [r for r in range(1, world) if sizes[r]]
+                    if src:
+                        eng.unpack_masked_ranks([rtiles[r] for r in src], W, H,
+                                                [recv_dev[q][int(roff[r]):].data_ptr() for r in src], nf,
+                                                images[q].data_ptr(), npx, stream=streams[q].cuda_stream)
                     if own:
                         images[q].index_copy_(0, dst_idx[off[0]:off[0] + nf * own], fbs[q][:nf * own])
                 return

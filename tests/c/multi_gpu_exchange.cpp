@@ -7,7 +7,7 @@
 //       PACKED (atr_render_start)
 //   wait_for_render_from_camera_to_finish (:457-471) -> atr_render_wait; per-tile ray_casts
 //       (atr_packed_tile_ray_casts); the pixels and the tile sums to rank 0 (grouped ncclSend /
-//       ncclRecv), rank 0 assembles the framebuffer (atr_unpack, or atr_unpack_masked for the
+//       ncclRecv), rank 0 assembles the framebuffer (atr_unpack, or atr_unpack_masked_ranks for the
 //       masked exchange) and sums total_ray_casts (:465-468)
 //
 // usage: multi_gpu_exchange OBJ W H SPP BOUNCES [--exchange u32|masked] [--side S] [--out FILE]
@@ -236,13 +236,23 @@ int main(int argc, char** argv) {
         ATR(atr_memset_d(ctx, d_image, 0x7F, size_t(W) * size_t(H) * 4));
         int64_t total_ray_casts = 0;
         std::vector<int64_t> grid_casts(size_t(ngrid), 0);  // RenderTile::ray_casts per grid tile
+        if (exchange == "masked") {  // every rank's stream in one call, positions from its tile blocks
+            std::vector<const atr_tile*> tp;
+            std::vector<int32_t> tn;
+            std::vector<const uint8_t*> pp;
+            for (int r = 0; r < world; ++r)
+                if (!tiles_of[size_t(r)].empty()) {
+                    tp.push_back(tiles_of[size_t(r)].data());
+                    tn.push_back(int32_t(tiles_of[size_t(r)].size()));
+                    pp.push_back(static_cast<const uint8_t*>(d_recv[size_t(r)]));
+                }
+            ATR(atr_unpack_masked_ranks(ctx, int32_t(tp.size()), tp.data(), tn.data(), W, H, pp.data(), 1, d_image,
+                                        int64_t(W) * H, nullptr));
+        }
         for (int r = 0; r < world; ++r) {
             const std::vector<atr_tile>& tr = tiles_of[size_t(r)];
             if (tr.empty()) continue;
-            if (exchange == "masked") {  // positions from rank r's tile blocks
-                ATR(atr_unpack_masked(ctx, tr.data(), int32_t(tr.size()), W, H, static_cast<const uint8_t*>(d_recv[size_t(r)]),
-                                      1, d_image, int64_t(W) * H, nullptr));
-            } else {
+            if (exchange != "masked") {
                 ATR(atr_unpack(ctx, tr.data(), int32_t(tr.size()), W, static_cast<const uint32_t*>(d_recv[size_t(r)]),
                                d_image, nullptr));
             }

@@ -645,7 +645,8 @@ def test_bgr_exchange_reassembles_frames(eng):
 
 @pytest.mark.parametrize("bgsel", ["sky", "first", "absent"])
 def test_masked_exchange_reassembles_frames(eng, bgsel):
-    """The masked exchange (atr_pack_bgr_masked / atr_scatter_bgr_masked / atr_unpack_masked, round 6): 3 ranks' packed
+    """The masked exchange (atr_pack_bgr_masked / atr_scatter_bgr_masked / atr_unpack_masked /
+    atr_unpack_masked_ranks, round 6): 3 ranks' packed
     shard frames (2 per launch) encoded against a background value -- the frame's common sky value,
     rank 0's first pixel, or a value no pixel has (every pixel then travels) -- decoded through the
     assembly index: every frame equals the full-frame render, the device stream equals the host
@@ -659,8 +660,10 @@ def test_masked_exchange_reassembles_frames(eng, bgsel):
     dst = torch.from_numpy(S.frames_assembly_index(plan, F)).cuda()
     img = torch.zeros(F * W * H, dtype=torch.int32, device="cuda")
     img2 = torch.full((F * (W * H + 5),), 0x7F7F7F7F, dtype=torch.int32, device="cuda")
+    img3 = torch.full((F * (W * H + 5),), 0x7F7F7F7F, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     bg = None
+    streams = []
     for r in range(world):
         n = plan.sizes[r]
         fb = torch.zeros(F * n, dtype=torch.int32, device="cuda")
@@ -682,13 +685,51 @@ def test_masked_exchange_reassembles_frames(eng, bgsel):
         eng.scatter_bgr_masked(out.data_ptr(), F * n, dst[off[r]:].data_ptr(), img.data_ptr(), stream=s)
         # and straight from the tile list's blocks (atr_unpack_masked), frames W * H + 5 apart
         eng.unpack_masked(plan.tiles[r], W, H, out.data_ptr(), F, img2.data_ptr(), W * H + 5, stream=s)
+        streams.append(out)
+    # and all ranks' streams in one call (atr_unpack_masked_ranks)
+    eng.unpack_masked_ranks(plan.tiles, W, H, [o.data_ptr() for o in streams], F, img3.data_ptr(), W * H + 5, stream=s)
     torch.cuda.synchronize()
+    assert torch.equal(img3, img2)
     for f in range(F):
         full = run(eng, cams[f])
         assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
         o = f * (W * H + 5)
         assert np.array_equal(img2[o:o + W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
         assert (img2[o + W * H:o + W * H + 5] == 0x7F7F7F7F).all()
+
+
+def test_unpack_masked_ranks_batches_past_sixteen_sources(eng):
+    """atr_unpack_masked_ranks with 20 sources (two launch pairs: 16 + 4), one of them holding no
+    pixel: the assembled frame equals the full-frame render."""
+    from atray_amd import shard as S
+    upload(eng, "Dragon", True)
+    W, H, world = 256, 160, 20
+    cam = E.camera(W, H, 1, 1)
+    plan = S.ShardPlan(W, H, world, 32)
+    full = run(eng, cam)
+    bg = S.background_value(full["fb"].ravel())
+    s = torch.cuda.current_stream().cuda_stream
+    tiles, outs = [], []
+    for r in range(world):
+        n = plan.sizes[r]
+        if not n:
+            continue
+        fb = torch.zeros(n, dtype=torch.int32, device="cuda")
+        eng.render_start(cam, plan.tiles[r], E.atr_frame(E.ATR_LAYOUT_PACKED, fb.data_ptr(), None, None, None, None,
+                                                         None), SEED, stream=s)
+        out = torch.zeros(E.pack_bgr_masked_bound(n), dtype=torch.uint8, device="cuda")
+        nb = torch.zeros(1, dtype=torch.int64, device="cuda")
+        eng.pack_bgr_masked(fb.data_ptr(), n, bg, out.data_ptr(), nb.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        tiles.append(plan.tiles[r])
+        outs.append(out)
+    assert len(tiles) > 16
+    tiles.append([[0, 0, -1, -1]])  # a source without pixels (an empty rect): skipped
+    outs.append(outs[0])
+    img = torch.full((W * H,), 0x7F7F7F7F, dtype=torch.int32, device="cuda")
+    eng.unpack_masked_ranks(tiles, W, H, [o.data_ptr() for o in outs], 1, img.data_ptr(), W * H, stream=s)
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])
 
 
 def test_block_cache_eviction_waits_for_every_stream(eng):
