@@ -17,7 +17,10 @@ Per repetition i and world N:
   T         max(end_last, rank 0's own span)
   speedup   full-frame ms per frame x frames / T; render side = full / slowest rank alone
 These are projections from one-GPU timings, not multi-GPU measurements.
-usage: python tools/project_r6.py DIR [cfg ...] > profiles/r06/projection.json"""
+With --assembly FILE (tools/assembly_probe.py's lines), rank 0's decode of a launch is the measured
+batched assembly (atr_unpack_masked_ranks + its own frames' copy) per frame of that world size,
+scaled by the frame's pixels against the probe's 1920x1080, instead of the byte model.
+usage: python tools/project_r6.py DIR [--assembly FILE] [cfg ...] > profiles/r06/projection.json"""
 import glob
 import json
 import os
@@ -35,11 +38,21 @@ def line(path):
 
 
 def main():
-    d = sys.argv[1]
-    cfgs = sys.argv[2:] or ["c3", "c4", "c5"]
+    args = sys.argv[1:]
+    asm = {}  # world -> measured assembly ms per 1920x1080 frame
+    if "--assembly" in args:
+        k = args.index("--assembly")
+        for ln in open(args[k + 1]):
+            if ln.startswith("{"):
+                a = json.loads(ln)
+                asm[int(a["world"])] = a["batched_ms"] / a["frames"]
+        del args[k:k + 2]
+    d = args[0]
+    cfgs = args[1:] or ["c3", "c4", "c5"]
     out = {"note": "projections from one-GPU shard timings with the masked exchange, not multi-GPU measurements",
-           "assumptions": {"xgmi_gbs_into_rank0": RATES, "decode_bytes_per_pixel": DECODE_BPP,
-                           "decode_tbs": HBM_TBS},
+           "assumptions": {"xgmi_gbs_into_rank0": RATES,
+                           "decode": ({"measured_assembly_ms_per_1080p_frame": {str(w): round(v, 5) for w, v in asm.items()}}
+                                      if asm else {"decode_bytes_per_pixel": DECODE_BPP, "decode_tbs": HBM_TBS})},
            "configs": {}}
     for cfg in cfgs:
         fulls = {}
@@ -76,8 +89,9 @@ def main():
                     for j, nf in enumerate(launches):
                         last = j == len(launches) - 1
                         ready = max(span[r] if last else done[r][j] for r in range(1, N))
-                        x = sum(bpf[r] for r in range(1, N)) * nf / (g * 1e9) * 1e3 + \
+                        dec = nf * asm[N] * W * H / (1920 * 1080) if N in asm else \
                             nf * W * H * DECODE_BPP / (HBM_TBS * 1e12) * 1e3
+                        x = sum(bpf[r] for r in range(1, N)) * nf / (g * 1e9) * 1e3 + dec
                         end = max(ready, end) + x
                     T = max(end, span[0])
                     rep_row["by_rate"][str(g)] = {"job_ms": round(T, 4), "speedup": round(full_ms * K / T, 3)}
