@@ -629,6 +629,7 @@ def run(args):
     hi_prio = torch.cuda.Stream.priority_range()[1] if args.stream_priority else 0
     streams = [torch.cuda.Stream(dev, priority=hi_prio if q == 0 else 0) for q in range(S_)]
     launch_ev = []  # per timed launch: (frames, event before its render, event after), launch order
+    launch_xev = []  # N > 1: per timed launch, an event after its exchange encoding (before the counters)
     own = W * H if pw == 1 else sizes[pr]  # output elements per frame (stride between frames)
     npx = W * H
     on_host = world > 1 and backend != "nccl"
@@ -777,6 +778,10 @@ def run(args):
                 if masked and own and pr != 0:  # the rank's frames as one masked stream (rank 0 keeps its own)
                     eng.pack_bgr_masked(fbs[q].data_ptr(), nf * own, bgv[0], enc[q].data_ptr(), nbytes[q].data_ptr(),
                                         stream=streams[q].cuda_stream)
+                if timing[0]:  # the launch's streams are ready to send from here
+                    ev_x = torch.cuda.Event(enable_timing=True)
+                    ev_x.record(streams[q])
+                    launch_xev.append(ev_x)
                 ts = tsum[q]
                 if rank == 0 and not sim:  # the reduction lands in rank 0's buffer: clear it; other
                     ts.zero_()             # ranks' stay zero outside their own tile columns
@@ -873,6 +878,7 @@ def run(args):
     launch_done = [round(ev0.elapsed_time(e), 3) for _, _, e in launch_ev]  # ms after the timed region's start
     launch_ms = [a.elapsed_time(e) for _, a, e in launch_ev]  # each timed launch's render, on its stream
     launch_frames = [nf for nf, _, _ in launch_ev]
+    launch_encoded = [round(ev0.elapsed_time(e), 3) for e in launch_xev]
     stream_bpf = None  # this rank's masked stream bytes per frame (the last launch of each stream)
     if masked and own and pr != 0:
         js = sorted(launch_nf)[-S_:]
@@ -998,7 +1004,9 @@ def run(args):
                               "bgr (3 B/px)" if bgr else "bgrx (4 B/px)"} if pw > 1 else {}),
                           "launches": launch_sizes(args.steps, F_, S_),
                           **({"rank0_extra": round(args.rank0_extra, 4)} if pw > 1 else {}),
-                          "launch_render_done_ms": launch_done, "stream_priority": bool(args.stream_priority),
+                          "launch_render_done_ms": launch_done,
+                          **({"launch_encoded_ms": launch_encoded} if launch_encoded else {}),
+                          "stream_priority": bool(args.stream_priority),
                           "cell_plan": cell_split,
                           "shard_pixels": [int(x) for x in sizes]},
                **({"sim": {"world": pw, "rank": pr, "note": "one rank's shard rendered alone, no exchange",

@@ -6,15 +6,15 @@ cost plan alone: bench.py --sim-world N --sim-rank r, which renders, counts and 
 that rank does in the N-GPU run, and reports its stream bytes per frame).
 
 Per repetition i and world N:
-  ready_j   launch j's streams are ready on every sender: the max over ranks of the launch's render
-            completion (launch_render_done_ms), the last launch at the rank's whole timed span
-            (render + counters + encoding)
+  ready_j   launch j's streams are ready on every sender: the max over ranks of the launch's encoding
+            done (launch_encoded_ms; older lines: the render's completion, the last launch at the
+            rank's whole timed span)
   x_j       rank 0 receives sum_r (stream bytes per frame of rank r) x frames_j at an assumed rate
             into rank 0 (200 / 350 / 500 GB/s: the 8-GPU node's rate is the driver's to measure),
             then decodes frames_j x W x H pixels (atr_unpack_masked: ~5.3 B of traffic per pixel at
             5 TB/s)
   end_j     max(ready_j, end_{j-1}) + x_j  (one exchange at a time into rank 0)
-  T         max(end_last, rank 0's own span)
+  T         max(end_last, every rank's whole span: render, encoding and per-tile counters)
   speedup   full-frame ms per frame x frames / T; render side = full / slowest rank alone
 These are projections from one-GPU timings, not multi-GPU measurements.
 With --assembly FILE (tools/assembly_probe.py's lines), rank 0's decode of a launch is the measured
@@ -77,6 +77,10 @@ def main():
                 span = {r: ln["ms_per_step"] * ln["steps"] for r, ln in ranks.items()}
                 launches = ranks[0]["config"]["launches"]
                 done = {r: ln["config"]["launch_render_done_ms"] for r, ln in ranks.items()}
+                # a launch's streams are ready once encoded (lines that record it); the per-tile
+                # counters that follow only feed the small reduction, so the job ends no earlier
+                # than every rank's whole span either
+                enc = {r: ln["config"].get("launch_encoded_ms") for r, ln in ranks.items()}
                 bpf = {r: (ln.get("sim") or {}).get("stream_bytes_per_frame") or 0 for r, ln in ranks.items()}
                 rep_row = {"full_ms_per_frame": full_ms,
                            "max_shard_ms_per_frame": round(max(span.values()) / K, 5),
@@ -88,12 +92,12 @@ def main():
                     end = 0.0
                     for j, nf in enumerate(launches):
                         last = j == len(launches) - 1
-                        ready = max(span[r] if last else done[r][j] for r in range(1, N))
+                        ready = max(enc[r][j] if enc[r] else (span[r] if last else done[r][j]) for r in range(1, N))
                         dec = nf * asm[N] * W * H / (1920 * 1080) if N in asm else \
                             nf * W * H * DECODE_BPP / (HBM_TBS * 1e12) * 1e3
                         x = sum(bpf[r] for r in range(1, N)) * nf / (g * 1e9) * 1e3 + dec
                         end = max(ready, end) + x
-                    T = max(end, span[0])
+                    T = max(end, max(span.values()))
                     rep_row["by_rate"][str(g)] = {"job_ms": round(T, 4), "speedup": round(full_ms * K / T, 3)}
                 reps.append(rep_row)
             if not reps:
