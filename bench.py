@@ -778,7 +778,7 @@ def run(args):
                 if masked and own and pr != 0:  # the rank's frames as one masked stream (rank 0 keeps its own)
                     eng.pack_bgr_masked(fbs[q].data_ptr(), nf * own, bgv[0], enc[q].data_ptr(), nbytes[q].data_ptr(),
                                         stream=streams[q].cuda_stream)
-                if timing[0]:  # the launch's streams are ready to send from here
+                if timing[0] and sim:  # the launch's streams are ready to send from here (projection)
                     ev_x = torch.cuda.Event(enable_timing=True)
                     ev_x.record(streams[q])
                     launch_xev.append(ev_x)
