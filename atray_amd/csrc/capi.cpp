@@ -50,9 +50,9 @@ extern "C" int64_t atr_masked_group_words(int64_t npixels);
 extern "C" int atr_unpack_max_sources();
 extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBlock* const* blocks,
                                                      const int32_t* nblocks, const int64_t* own,
-                                                     const uint8_t* const* in, int32_t width, int32_t nframes,
-                                                     uint32_t* image, int64_t image_stride, uint32_t* goff,
-                                                     hipStream_t s);
+                                                     const uint8_t* const* in, const int32_t* raw, int32_t width,
+                                                     int32_t nframes, uint32_t* image, int64_t image_stride,
+                                                     uint32_t* goff, hipStream_t s);
 extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                                const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
                                                int64_t image_stride, uint32_t* goff, hipStream_t s);
@@ -1913,8 +1913,8 @@ int atr_unpack_masked(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t
 }
 
 int atr_unpack_masked_ranks(atr_ctx* c, int32_t nsrc, const atr_tile* const* tiles, const int32_t* ntiles,
-                            int32_t width, int32_t height, const uint8_t* const* packed, int32_t nframes,
-                            uint32_t* image, int64_t image_stride, void* stream) {
+                            int32_t width, int32_t height, const uint8_t* const* packed, const int32_t* raw,
+                            int32_t nframes, uint32_t* image, int64_t image_stride, void* stream) {
     if (!c || nsrc < 0 || (nsrc && (!tiles || !ntiles || !packed)) || !image || width <= 0 || height <= 0 ||
         nframes < 0 || image_stride < int64_t(width) * height)
         return ATR_E_INVALID;
@@ -1940,14 +1940,14 @@ int atr_unpack_masked_ranks(atr_ctx* c, int32_t nsrc, const atr_tile* const* til
             nb[size_t(k)] = int32_t(bs->host.size());
             own[size_t(k)] = bs->packed_pixels;
             if (int64_t(nframes) * own[size_t(k)] >= (int64_t(1) << 32)) return ATR_E_INVALID;
-            words += atr_masked_group_words(int64_t(nframes) * own[size_t(k)]);
+            if (!(raw && raw[i0 + k])) words += atr_masked_group_words(int64_t(nframes) * own[size_t(k)]);
         }
-        if (words == 0) continue;
-        void* goff = nullptr;
-        HIPCHK(hipMallocAsync(&goff, sizeof(uint32_t) * size_t(words), s));
-        HIPCHK(atr_launch_unpack_masked_multi(n, blocks.data(), nb.data(), own.data(), packed + i0, width, nframes,
-                                              image, image_stride, static_cast<uint32_t*>(goff), s));
-        HIPCHK(hipFreeAsync(goff, s));
+        void* goff = nullptr;  // the group offsets of the masked sources (none for raw ones)
+        if (words) HIPCHK(hipMallocAsync(&goff, sizeof(uint32_t) * size_t(words), s));
+        HIPCHK(atr_launch_unpack_masked_multi(n, blocks.data(), nb.data(), own.data(), packed + i0,
+                                              raw ? raw + i0 : nullptr, width, nframes, image, image_stride,
+                                              static_cast<uint32_t*>(goff), s));
+        if (goff) HIPCHK(hipFreeAsync(goff, s));
     }
     HIPCHK(note_launch(c, s));
     return ATR_OK;

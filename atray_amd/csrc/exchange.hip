@@ -188,7 +188,8 @@ struct UnpackSrc {
     int64_t nchunk;  // the stream's chunks
     int64_t chunk0;  // its first chunk in the group-offset grid (its group words at chunk0 * 128)
     int64_t wave0;   // its first wave (block) in the decode grid
-    int32_t nblocks, pad;
+    int32_t nblocks;
+    int32_t raw;     // 1: `in` is the render's u32 PACKED frames themselves (rank 0's own), no stream
 };
 struct UnpackSrcs {
     UnpackSrc s[kMaxUnpackSrc];
@@ -241,12 +242,17 @@ __global__ __launch_bounds__(256) void unpack_masked_kernel(UnpackSrcs S, int64_
     if (!((mask >> lane) & 1)) return;
     const uint8_t* __restrict__ in = src.in;
     const int64_t nchunk = src.nchunk, own = src.own;
+    const int64_t slot0 = blk.out_base + __popcll(mask & ((uint64_t(1) << lane) - 1));
+    uint32_t* dst = image + int64_t(blk.y0 + (lane >> 3)) * width + blk.x0 + (lane & 7);
+    if (src.raw) {  // a copy of the packed frames into the image
+        const uint32_t* __restrict__ fb = reinterpret_cast<const uint32_t*>(in);
+        for (int32_t f = 0; f < nframes; ++f) dst[int64_t(f) * image_stride] = fb[int64_t(f) * own + slot0];
+        return;
+    }
     const uint32_t bg = reinterpret_cast<const uint32_t*>(in)[1];
     const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk);
     const uint8_t* pay = in + 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk;
     const uint32_t* __restrict__ goff = goff_all + src.chunk0 * (kMaskChunk / 64);
-    const int64_t slot0 = blk.out_base + __popcll(mask & ((uint64_t(1) << lane) - 1));
-    uint32_t* dst = image + int64_t(blk.y0 + (lane >> 3)) * width + blk.x0 + (lane & 7);
     for (int32_t f0 = 0; f0 < nframes; f0 += kUnpackFrames) {
         uint64_t m[kUnpackFrames];
         uint32_t go[kUnpackFrames];
@@ -321,17 +327,19 @@ extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n
 extern "C" int atr_unpack_max_sources() { return atr::kMaxUnpackSrc; }
 extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBlock* const* blocks,
                                                      const int32_t* nblocks, const int64_t* own,
-                                                     const uint8_t* const* in, int32_t width, int32_t nframes,
-                                                     uint32_t* image, int64_t image_stride, uint32_t* goff,
-                                                     hipStream_t s) {
+                                                     const uint8_t* const* in, const int32_t* raw, int32_t width,
+                                                     int32_t nframes, uint32_t* image, int64_t image_stride,
+                                                     uint32_t* goff, hipStream_t s) {
     if (n <= 0 || n > atr::kMaxUnpackSrc || nframes <= 0) return n > atr::kMaxUnpackSrc ? hipErrorInvalidValue : hipSuccess;
     atr::UnpackSrcs S;
     std::memset(&S, 0, sizeof(S));
     int64_t chunks = 0, waves = 0;
     for (int32_t i = 0; i < n; ++i) {
         atr::UnpackSrc& u = S.s[S.n];
-        const int64_t nc = atr_masked_chunks(int64_t(nframes) * own[i]);
-        if (nc <= 0 || nblocks[i] <= 0) continue;  // nothing to decode from this source
+        const bool r = raw && raw[i];
+        const int64_t nc = r ? 0 : atr_masked_chunks(int64_t(nframes) * own[i]);
+        if ((!r && nc <= 0) || nblocks[i] <= 0 || own[i] <= 0) continue;  // nothing to decode from this source
+        u.raw = r ? 1 : 0;
         u.blocks = blocks[i];
         u.in = in[i];
         u.own = own[i];
@@ -344,9 +352,11 @@ extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBloc
         ++S.n;
     }
     if (!S.n) return hipSuccess;
-    hipLaunchKernelGGL(atr::masked_group_offsets_kernel, dim3(unsigned(chunks)), dim3(128), 0, s, S, goff);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (chunks > 0) {
+        hipLaunchKernelGGL(atr::masked_group_offsets_kernel, dim3(unsigned(chunks)), dim3(128), 0, s, S, goff);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(atr::unpack_masked_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, s, S, waves, width,
                        goff, nframes, image, image_stride);
     return hipGetLastError();
@@ -355,7 +365,8 @@ extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBloc
 extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                                const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
                                                int64_t image_stride, uint32_t* goff, hipStream_t s) {
-    return atr_launch_unpack_masked_multi(1, &blocks, &nblocks, &own, &in, width, nframes, image, image_stride, goff, s);
+    return atr_launch_unpack_masked_multi(1, &blocks, &nblocks, &own, &in, nullptr, width, nframes, image, image_stride,
+                                          goff, s);
 }
 
 extern "C" int64_t atr_masked_group_words(int64_t npixels) { return atr_masked_chunks(npixels) * (atr::kMaskChunk / 64); }

@@ -183,7 +183,7 @@ def lib():
         "atr_pack_bgr_masked": ([vp, vp, i64, u32, vp, vp, vp], C.c_int),
         "atr_scatter_bgr_masked": ([vp, vp, i64, vp, vp, vp], C.c_int),
         "atr_unpack_masked": ([vp, vp, i32, i32, i32, vp, i32, vp, i64, vp], C.c_int),
-        "atr_unpack_masked_ranks": ([vp, i32, vp, vp, i32, i32, vp, i32, vp, i64, vp], C.c_int),
+        "atr_unpack_masked_ranks": ([vp, i32, vp, vp, i32, i32, vp, vp, i32, vp, i64, vp], C.c_int),
         "atr_render_simd_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_path_counters": ([vp, P(atr_camera), vp, i32, C.c_uint64, i32, vp], C.c_int),
         "atr_render_cell_costs": ([vp, P(atr_camera), C.c_uint64, i32, vp], C.c_int),
@@ -595,15 +595,17 @@ class Engine:
                                       C.c_void_p(stream) if stream else None), "unpack masked")
 
     def unpack_masked_ranks(self, tiles_list, width, height, packed_ptrs, nframes, image_ptr, image_stride,
-                            stream=None):
+                            stream=None, raw=None):
         """Several masked streams (source i: the PACKED render of tiles_list[i], its stream at
-        packed_ptrs[i]) into the same IMAGE frames in one call (atr_unpack_masked_ranks)."""
+        packed_ptrs[i]; with raw[i] true, that render's u32 PACKED frames themselves) into the same
+        IMAGE frames in one call (atr_unpack_masked_ranks)."""
         arrs = [t if isinstance(t, tuple) else tiles_array(t) for t in tiles_list]
         n = len(arrs)
         tp = (C.c_void_p * max(1, n))(*[C.cast(a, C.c_void_p) for a, _ in arrs])
         nt = (C.c_int32 * max(1, n))(*[k for _, k in arrs])
         pp = (C.c_void_p * max(1, n))(*[int(p) for p in packed_ptrs])
-        check(lib().atr_unpack_masked_ranks(self.h, n, tp, nt, int(width), int(height), pp, int(nframes),
+        rw = (C.c_int32 * max(1, n))(*[int(bool(x)) for x in raw]) if raw is not None else None
+        check(lib().atr_unpack_masked_ranks(self.h, n, tp, nt, int(width), int(height), pp, rw, int(nframes),
                                             C.c_void_p(image_ptr), int(image_stride),
                                             C.c_void_p(stream) if stream else None), "unpack masked ranks")
 

@@ -735,15 +735,15 @@ def run(args):
                 if rank == 0:
                     if on_host:
                         recv_dev[q].copy_(recv[q])
-                    # every other rank's stream in one call, positions from its tile blocks
-                    # (atr_unpack_masked_ranks: one launch pair instead of two launches per rank)
+                    # every other rank's stream and rank 0's own packed frames in one call,
+                    # positions from each source's tile blocks (atr_unpack_masked_ranks: one
+                    # launch pair instead of two launches per rank and an index copy)
                     src = [r for r in range(1, world) if sizes[r]]
-                    if src:
-                        eng.unpack_masked_ranks([rtiles[r] for r in src], W, H,
-                                                [recv_dev[q][int(roff[r]):].data_ptr() for r in src], nf,
-                                                images[q].data_ptr(), npx, stream=streams[q].cuda_stream)
-                    if own:
-                        images[q].index_copy_(0, dst_idx[off[0]:off[0] + nf * own], fbs[q][:nf * own])
+                    tl = [rtiles[r] for r in src] + ([rtiles[0]] if own else [])
+                    ptrs = [recv_dev[q][int(roff[r]):].data_ptr() for r in src] + ([fbs[q].data_ptr()] if own else [])
+                    if tl:
+                        eng.unpack_masked_ranks(tl, W, H, ptrs, nf, images[q].data_ptr(), npx,
+                                                stream=streams[q].cuda_stream, raw=[0] * len(src) + [1] * (1 if own else 0))
                 return
             if rank == 0 and bgr:
                 if on_host:

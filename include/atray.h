@@ -344,13 +344,14 @@ int atr_unpack_masked(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32
                       const uint8_t* packed, int32_t nframes, uint32_t* image, int64_t image_stride, void* stream);
 /* Several masked streams into the same IMAGE frames in one call (rank 0's received shards, one
    source per rank): source i is the PACKED render of tiles[i] (ntiles[i] tiles, the list it was
-   rendered with), its stream at packed[i] (device), nframes frames each, image_stride apart. The
-   same pixels as atr_unpack_masked per source, from one group-offset and one decode launch per 16
-   sources instead of two launches, an allocation and an event per source. Asynchronous on
-   `stream`. */
+   rendered with), its stream at packed[i] (device), nframes frames each, image_stride apart; with
+   raw[i] nonzero (raw may be NULL) packed[i] is that render's u32 PACKED framebuffer itself (rank
+   0's own frames), copied in by the same launch. The same pixels as atr_unpack_masked (or
+   atr_unpack) per source, from one group-offset and one decode launch per 16 sources instead of two
+   launches, an allocation and an event per source. Asynchronous on `stream`. */
 int atr_unpack_masked_ranks(atr_ctx* ctx, int32_t nsrc, const atr_tile* const* tiles, const int32_t* ntiles,
-                            int32_t width, int32_t height, const uint8_t* const* packed, int32_t nframes,
-                            uint32_t* image, int64_t image_stride, void* stream);
+                            int32_t width, int32_t height, const uint8_t* const* packed, const int32_t* raw,
+                            int32_t nframes, uint32_t* image, int64_t image_stride, void* stream);
 /* Per-cell launch plan for renders of width x height (NULL clears): one byte per 8x8 cell (row
    major, ceil(W/8) x ceil(H/8)). Low nibble: the number of waves the cell is split into (0/1 =
    one, 2, 4 or 8 row bands: a heavy cell's rays then share their dealt leaf scans with 2-8x as

@@ -246,8 +246,8 @@ int main(int argc, char** argv) {
                     tn.push_back(int32_t(tiles_of[size_t(r)].size()));
                     pp.push_back(static_cast<const uint8_t*>(d_recv[size_t(r)]));
                 }
-            ATR(atr_unpack_masked_ranks(ctx, int32_t(tp.size()), tp.data(), tn.data(), W, H, pp.data(), 1, d_image,
-                                        int64_t(W) * H, nullptr));
+            ATR(atr_unpack_masked_ranks(ctx, int32_t(tp.size()), tp.data(), tn.data(), W, H, pp.data(), nullptr, 1,
+                                        d_image, int64_t(W) * H, nullptr));
         }
         for (int r = 0; r < world; ++r) {
             const std::vector<atr_tile>& tr = tiles_of[size_t(r)];

@@ -670,6 +670,8 @@ def test_masked_exchange_reassembles_frames(eng, bgsel):
         fr = E.atr_frame(E.ATR_LAYOUT_PACKED, fb.data_ptr(), None, None, None, None, None)
         eng.render_start_cameras(cams, plan.tiles[r], fr, n, SEED, stream=s)
         torch.cuda.synchronize()
+        if r == 0:
+            fb0 = fb
         host = fb.cpu().numpy().view(np.uint32)
         if bg is None:
             bg = {"sky": S.background_value(host), "first": int(host[0]), "absent": 0x01000000}[bgsel]
@@ -686,10 +688,14 @@ def test_masked_exchange_reassembles_frames(eng, bgsel):
         # and straight from the tile list's blocks (atr_unpack_masked), frames W * H + 5 apart
         eng.unpack_masked(plan.tiles[r], W, H, out.data_ptr(), F, img2.data_ptr(), W * H + 5, stream=s)
         streams.append(out)
-    # and all ranks' streams in one call (atr_unpack_masked_ranks)
+    # and all ranks' streams in one call (atr_unpack_masked_ranks); then ranks 1.. as streams and
+    # rank 0 as its raw packed frames
     eng.unpack_masked_ranks(plan.tiles, W, H, [o.data_ptr() for o in streams], F, img3.data_ptr(), W * H + 5, stream=s)
+    img4 = torch.full_like(img3, 0x7F7F7F7F)
+    eng.unpack_masked_ranks(plan.tiles[1:] + [plan.tiles[0]], W, H, [o.data_ptr() for o in streams[1:]] + [fb0.data_ptr()],
+                            F, img4.data_ptr(), W * H + 5, stream=s, raw=[0] * (world - 1) + [1])
     torch.cuda.synchronize()
-    assert torch.equal(img3, img2)
+    assert torch.equal(img3, img2) and torch.equal(img4, img2)
     for f in range(F):
         full = run(eng, cams[f])
         assert np.array_equal(img[f * W * H:(f + 1) * W * H].cpu().numpy().view(np.uint32).reshape(H, W), full["fb"])

@@ -2,8 +2,8 @@
 c3 cost plan is rendered and encoded here (the masked stream, as that rank would send it), then
 rank 0's per-launch assembly -- decode every other rank's stream into the images and copy its own
 frames in -- is timed with HIP events on an otherwise idle GPU (median of repeats). Compares the
-per-rank decode calls (atr_unpack_masked, one per rank) with the batched call
-(atr_unpack_masked_ranks, one for all ranks) when the library has it; checks that both assemble
+per-rank decode calls (atr_unpack_masked, one per rank, and an index copy of rank 0's own frames)
+with the batched call (atr_unpack_masked_ranks: every rank's stream and rank 0's own frames); checks that both assemble
 the same images as a one-launch full-frame render. Prints one JSON line per world size.
 
 python tools/assembly_probe.py [worlds, e.g. 2,4,8] [frames]"""
@@ -66,11 +66,10 @@ def probe(world):
             eng.unpack_masked(tiles[r], W, H, encs[r].data_ptr(), F, images.data_ptr(), npx, stream=s.cuda_stream)
         images.index_copy_(0, dst0, fbs[0])
 
-    def assemble_batched():
-        eng.unpack_masked_ranks([tiles[r] for r in range(1, world)], W, H,
-                                [encs[r].data_ptr() for r in range(1, world)], F, images.data_ptr(), npx,
-                                stream=s.cuda_stream)
-        images.index_copy_(0, dst0, fbs[0])
+    def assemble_batched():  # rank 0's own packed frames as a raw source of the same launch
+        eng.unpack_masked_ranks([tiles[r] for r in range(1, world)] + [tiles[0]], W, H,
+                                [encs[r].data_ptr() for r in range(1, world)] + [fbs[0].data_ptr()], F,
+                                images.data_ptr(), npx, stream=s.cuda_stream, raw=[0] * (world - 1) + [1])
 
     def timed(fn, n=20):
         ms = []
