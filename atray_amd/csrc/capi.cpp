@@ -46,16 +46,15 @@ extern "C" hipError_t atr_launch_plan(const atr::DBlock* base, int32_t nb, unsig
 extern "C" size_t atr_plan_work_bytes(int32_t nb);
 extern "C" hipError_t atr_launch_pack_bgr(const uint32_t* src, int64_t n, uint8_t* dst, hipStream_t s);
 extern "C" int64_t atr_masked_chunks(int64_t n);
-extern "C" int64_t atr_masked_group_words(int64_t npixels);
 extern "C" int atr_unpack_max_sources();
 extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBlock* const* blocks,
                                                      const int32_t* nblocks, const int64_t* own,
                                                      const uint8_t* const* in, const int32_t* raw, int32_t width,
                                                      int32_t nframes, uint32_t* image, int64_t image_stride,
-                                                     uint32_t* goff, hipStream_t s);
+                                                     hipStream_t s);
 extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                                const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
-                                               int64_t image_stride, uint32_t* goff, hipStream_t s);
+                                               int64_t image_stride, hipStream_t s);
 extern "C" hipError_t atr_launch_pack_bgr_masked(const uint32_t* src, int64_t n, uint32_t bg, uint8_t* out,
                                                  int64_t* nbytes, hipStream_t s);
 extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n, const int64_t* dst_index,
@@ -1869,7 +1868,7 @@ int atr_scatter_bgr(atr_ctx* c, const uint8_t* packed, int64_t npixels, const in
 int64_t atr_pack_bgr_masked_bound(int64_t npixels) {
     if (npixels < 0) return ATR_E_INVALID;
     const int64_t nc = atr_masked_chunks(npixels);
-    return 16 + 4 * nc + 1024 * nc + 3 * npixels;
+    return 16 + 4 * nc + 1024 * nc + 512 * nc + 3 * npixels;  // header, chunk offsets, masks, group offsets
 }
 
 int atr_pack_bgr_masked(atr_ctx* c, const uint32_t* framebuffer, int64_t npixels, uint32_t background, uint8_t* out,
@@ -1903,11 +1902,8 @@ int atr_unpack_masked(atr_ctx* c, const atr_tile* tiles, int32_t ntiles, int32_t
     if (nframes == 0 || own == 0) return ATR_OK;
     if (int64_t(nframes) * own >= (int64_t(1) << 32)) return ATR_E_INVALID;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream (HIP convention)
-    void* goff = nullptr;
-    HIPCHK(hipMallocAsync(&goff, sizeof(uint32_t) * size_t(atr_masked_group_words(int64_t(nframes) * own)), s));
     HIPCHK(atr_launch_unpack_masked(static_cast<const DBlock*>(bs->dev.p), int32_t(bs->host.size()), width, packed,
-                                    nframes, own, image, image_stride, static_cast<uint32_t*>(goff), s));
-    HIPCHK(hipFreeAsync(goff, s));
+                                    nframes, own, image, image_stride, s));
     HIPCHK(note_launch(c, s));
     return ATR_OK;
 }
@@ -1929,7 +1925,6 @@ int atr_unpack_masked_ranks(atr_ctx* c, int32_t nsrc, const atr_tile* const* til
         std::vector<const DBlock*> blocks(size_t(n), nullptr);
         std::vector<int32_t> nb(size_t(n), 0);
         std::vector<int64_t> own(size_t(n), 0);
-        int64_t words = 0;
         for (int32_t k = 0; k < n; ++k) {
             int rc = ATR_OK;
             // the renders' cached sets (the most recently used slots: a later lookup here does not
@@ -1940,14 +1935,9 @@ int atr_unpack_masked_ranks(atr_ctx* c, int32_t nsrc, const atr_tile* const* til
             nb[size_t(k)] = int32_t(bs->host.size());
             own[size_t(k)] = bs->packed_pixels;
             if (int64_t(nframes) * own[size_t(k)] >= (int64_t(1) << 32)) return ATR_E_INVALID;
-            if (!(raw && raw[i0 + k])) words += atr_masked_group_words(int64_t(nframes) * own[size_t(k)]);
         }
-        void* goff = nullptr;  // the group offsets of the masked sources (none for raw ones)
-        if (words) HIPCHK(hipMallocAsync(&goff, sizeof(uint32_t) * size_t(words), s));
         HIPCHK(atr_launch_unpack_masked_multi(n, blocks.data(), nb.data(), own.data(), packed + i0,
-                                              raw ? raw + i0 : nullptr, width, nframes, image, image_stride,
-                                              static_cast<uint32_t*>(goff), s));
-        if (goff) HIPCHK(hipFreeAsync(goff, s));
+                                              raw ? raw + i0 : nullptr, width, nframes, image, image_stride, s));
     }
     HIPCHK(note_launch(c, s));
     return ATR_OK;

@@ -36,17 +36,23 @@ __global__ __launch_bounds__(256) void scatter_bgr_kernel(const uint8_t* __restr
 // ---------------------------------------------------------------- masked (background) exchange
 // Lossless, for frames that are mostly one value (c3: 86% of the pixels are the sky's colour): a
 // bit per pixel "not the background" plus 3 bytes for each such pixel only. Stream layout (bytes):
-//   [0, 16)        magic 'ATRM', bg (BGRX u32), nchunk, payload pixels in all
+//   [0, 16)        magic 'ATRN', bg (BGRX u32), nchunk, payload pixels in all
 //   [16, +4 n)     payload pixel offset of each 8192-pixel chunk (exclusive prefix)
 //   then           256 mask words (u32) per chunk, bit i of word k = pixel 32 k + i of the chunk
+//   then           128 group offsets (u32) per chunk: the payload pixel offset of each 64-pixel
+//                  group (written by the encoder, so a decoder needs no scan of its own)
 //   then           3 bytes (B, G, R) per non-background pixel, in pixel order
 // Encoder: masks and per-chunk counts (one ballot per 64 pixels), the counts' scan (one
-// workgroup), the payload; decoder: one pass, each wave deriving its offset from the masks.
+// workgroup), the payload and group offsets; decoders: one pass.
 constexpr int kMaskChunk = 8192;  // pixels per chunk = 4 waves x 32 groups of 64
-constexpr uint32_t kMaskMagic = 0x4D525441u;  // "ATRM"
+constexpr uint32_t kMaskMagic = 0x4E525441u;  // "ATRN" (round 6's first layout, "ATRM", had no group offsets)
 
 __device__ __forceinline__ uint32_t* mask_words(uint8_t* base, int64_t nchunk) {
     return reinterpret_cast<uint32_t*>(base + 16 + 4 * nchunk);
+}
+__device__ __forceinline__ int64_t group_offsets_at(int64_t nchunk) { return 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk; }
+__device__ __forceinline__ int64_t payload_at(int64_t nchunk) {
+    return group_offsets_at(nchunk) + int64_t(kMaskChunk / 64) * 4 * nchunk;
 }
 
 // Wave w of chunk c covers pixels c * 8192 + w * 2048 + [0, 2048): 32 groups of 64.
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(1024) void masked_scan_kernel(uint8_t* __restrict__
         h[1] = bg;
         h[2] = uint32_t(nchunk);
         h[3] = carry_s;
-        *nbytes = 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk + 3 * int64_t(carry_s);
+        *nbytes = payload_at(nchunk) + 3 * int64_t(carry_s);
     }
 }
 
@@ -130,10 +136,12 @@ __global__ __launch_bounds__(256) void masked_payload_kernel(const uint32_t* __r
     const int64_t c = blockIdx.x;
     const uint32_t* mw = mask_words(out, nchunk) + c * (kMaskChunk / 32);
     uint32_t base = masked_wave_base(reinterpret_cast<const uint32_t*>(out + 16), mw, w, ln);
-    uint8_t* pay = reinterpret_cast<uint8_t*>(mask_words(out, nchunk) + nchunk * (kMaskChunk / 32));
+    uint8_t* pay = out + payload_at(nchunk);
+    uint32_t* gw = reinterpret_cast<uint32_t*>(out + group_offsets_at(nchunk)) + c * (kMaskChunk / 64) + w * 32;
     const int64_t p0 = c * kMaskChunk + int64_t(w) * 2048;
     const unsigned long long below = (ln ? ~0ull >> (64 - ln) : 0ull);
     for (int g = 0; g < 32; ++g) {
+        if (ln == 0) gw[g] = base;  // the group's first payload pixel
         const unsigned long long m = uint64_t(mw[w * 64 + 2 * g]) | (uint64_t(mw[w * 64 + 2 * g + 1]) << 32);
         if ((m >> ln) & 1) {
             const uint32_t v = src[p0 + g * 64 + ln];
@@ -154,7 +162,7 @@ __global__ __launch_bounds__(256) void masked_scatter_kernel(const uint8_t* __re
     const uint32_t bg = reinterpret_cast<const uint32_t*>(in)[1];
     const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk) + c * (kMaskChunk / 32);
     uint32_t base = masked_wave_base(reinterpret_cast<const uint32_t*>(in + 16), mw, w, ln);
-    const uint8_t* pay = in + 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk;
+    const uint8_t* pay = in + payload_at(nchunk);
     const int64_t p0 = c * kMaskChunk + int64_t(w) * 2048;
     const unsigned long long below = (ln ? ~0ull >> (64 - ln) : 0ull);
     for (int g = 0; g < 32; ++g) {
@@ -175,18 +183,17 @@ __global__ __launch_bounds__(256) void masked_scatter_kernel(const uint8_t* __re
 
 // Block-structured decode (atr_unpack_masked, atr_unpack_masked_ranks): the stream of a PACKED
 // render of a tile list is in its blocks' slot order, so each 8x8 block's wave finds its pixels'
-// image positions from the block record (32 B per 64 pixels) instead of an 8-B index per pixel.
-// Each 64-slot group's first payload pixel comes from a per-chunk scan of the mask popcounts
-// (masked_group_offsets_kernel). One launch pair decodes up to kMaxUnpackSrc streams (rank 0's
-// received shards): the grids are the sources' chunks and waves back to back, each workgroup or
-// wave finding its source in the kernel-argument table.
+// image positions from the block record (32 B per 64 pixels) instead of an 8-B index per pixel,
+// and each 64-slot group's first payload pixel in the stream's group offsets. One launch decodes
+// up to kMaxUnpackSrc streams (rank 0's received shards, and its own packed frames as a raw
+// source): the grid is the sources' blocks back to back, each wave finding its source in the
+// kernel-argument table.
 constexpr int kMaxUnpackSrc = 16;
 struct UnpackSrc {
     const DBlock* blocks;
     const uint8_t* in;
     int64_t own;     // packed pixels per frame
     int64_t nchunk;  // the stream's chunks
-    int64_t chunk0;  // its first chunk in the group-offset grid (its group words at chunk0 * 128)
     int64_t wave0;   // its first wave (block) in the decode grid
     int32_t nblocks;
     int32_t raw;     // 1: `in` is the render's u32 PACKED frames themselves (rank 0's own), no stream
@@ -196,32 +203,6 @@ struct UnpackSrcs {
     int32_t n, pad;
 };
 
-__device__ __forceinline__ int unpack_src_of_chunk(const UnpackSrcs& S, int64_t c) {
-    int i = 0;
-    while (i + 1 < S.n && c >= S.s[i + 1].chunk0) ++i;
-    return i;
-}
-
-__global__ __launch_bounds__(128) void masked_group_offsets_kernel(UnpackSrcs S, uint32_t* __restrict__ goff) {
-    __shared__ uint32_t wsum[2];
-    const int si = unpack_src_of_chunk(S, int64_t(blockIdx.x));
-    const UnpackSrc& src = S.s[si];
-    const uint8_t* in = src.in;
-    const int64_t nchunk = src.nchunk, c = int64_t(blockIdx.x) - src.chunk0;
-    const int t = threadIdx.x, ln = t & 63, w = t >> 6;
-    const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk) + c * (kMaskChunk / 32);
-    const uint32_t v = uint32_t(__popc(mw[2 * t]) + __popc(mw[2 * t + 1]));
-    uint32_t x = v;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = uint32_t(__shfl_up(int(x), d));
-        if (ln >= d) x += y;
-    }
-    if (ln == 63) wsum[w] = x;
-    __syncthreads();
-    goff[int64_t(blockIdx.x) * (kMaskChunk / 64) + t] =
-        reinterpret_cast<const uint32_t*>(in + 16)[c] + (w ? wsum[0] : 0u) + x - v;
-}
-
 // One wave per (source, block), looping over the frames kUnpackFrames at a time with their loads
 // issued together (mask words and group offset, then payload bytes, then the stores): the block
 // record is read once for all frames and no item index has to be divided into frame and block
@@ -229,8 +210,8 @@ __global__ __launch_bounds__(128) void masked_group_offsets_kernel(UnpackSrcs S,
 // three dependent loads per 64 pixels dominating).
 constexpr int kUnpackFrames = 4;
 __global__ __launch_bounds__(256) void unpack_masked_kernel(UnpackSrcs S, int64_t nblocks_all, int32_t width,
-                                                            const uint32_t* __restrict__ goff_all, int32_t nframes,
-                                                            uint32_t* __restrict__ image, int64_t image_stride) {
+                                                            int32_t nframes, uint32_t* __restrict__ image,
+                                                            int64_t image_stride) {
     const int64_t wv = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (wv >= nblocks_all) return;
@@ -251,8 +232,8 @@ __global__ __launch_bounds__(256) void unpack_masked_kernel(UnpackSrcs S, int64_
     }
     const uint32_t bg = reinterpret_cast<const uint32_t*>(in)[1];
     const uint32_t* mw = reinterpret_cast<const uint32_t*>(in + 16 + 4 * nchunk);
-    const uint8_t* pay = in + 16 + 4 * nchunk + int64_t(kMaskChunk / 8) * nchunk;
-    const uint32_t* __restrict__ goff = goff_all + src.chunk0 * (kMaskChunk / 64);
+    const uint8_t* pay = in + payload_at(nchunk);
+    const uint32_t* __restrict__ goff = reinterpret_cast<const uint32_t*>(in + group_offsets_at(nchunk));
     for (int32_t f0 = 0; f0 < nframes; f0 += kUnpackFrames) {
         uint64_t m[kUnpackFrames];
         uint32_t go[kUnpackFrames];
@@ -322,18 +303,17 @@ extern "C" hipError_t atr_launch_scatter_bgr_masked(const uint8_t* in, int64_t n
 }
 
 // Up to kMaxUnpackSrc streams into the same frames: blocks[i] (nblocks[i] blocks of a PACKED
-// render, own[i] pixels per frame), in[i] its stream; goff: sum over i of atr_masked_group_words(
-// nframes x own[i]) words of scratch.
+// render, own[i] pixels per frame), in[i] its stream (or, raw[i], its u32 PACKED frames).
 extern "C" int atr_unpack_max_sources() { return atr::kMaxUnpackSrc; }
 extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBlock* const* blocks,
                                                      const int32_t* nblocks, const int64_t* own,
                                                      const uint8_t* const* in, const int32_t* raw, int32_t width,
                                                      int32_t nframes, uint32_t* image, int64_t image_stride,
-                                                     uint32_t* goff, hipStream_t s) {
+                                                     hipStream_t s) {
     if (n <= 0 || n > atr::kMaxUnpackSrc || nframes <= 0) return n > atr::kMaxUnpackSrc ? hipErrorInvalidValue : hipSuccess;
     atr::UnpackSrcs S;
     std::memset(&S, 0, sizeof(S));
-    int64_t chunks = 0, waves = 0;
+    int64_t waves = 0;
     for (int32_t i = 0; i < n; ++i) {
         atr::UnpackSrc& u = S.s[S.n];
         const bool r = raw && raw[i];
@@ -344,29 +324,21 @@ extern "C" hipError_t atr_launch_unpack_masked_multi(int32_t n, const atr::DBloc
         u.in = in[i];
         u.own = own[i];
         u.nchunk = nc;
-        u.chunk0 = chunks;
         u.wave0 = waves;  // its first block in the decode grid (a wave per block)
         u.nblocks = nblocks[i];
-        chunks += nc;
         waves += nblocks[i];
         ++S.n;
     }
     if (!S.n) return hipSuccess;
-    if (chunks > 0) {
-        hipLaunchKernelGGL(atr::masked_group_offsets_kernel, dim3(unsigned(chunks)), dim3(128), 0, s, S, goff);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
     hipLaunchKernelGGL(atr::unpack_masked_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, s, S, waves, width,
-                       goff, nframes, image, image_stride);
+                       nframes, image, image_stride);
     return hipGetLastError();
 }
 
 extern "C" hipError_t atr_launch_unpack_masked(const atr::DBlock* blocks, int32_t nblocks, int32_t width,
                                                const uint8_t* in, int32_t nframes, int64_t own, uint32_t* image,
-                                               int64_t image_stride, uint32_t* goff, hipStream_t s) {
+                                               int64_t image_stride, hipStream_t s) {
     return atr_launch_unpack_masked_multi(1, &blocks, &nblocks, &own, &in, nullptr, width, nframes, image, image_stride,
-                                          goff, s);
+                                          s);
 }
 
-extern "C" int64_t atr_masked_group_words(int64_t npixels) { return atr_masked_chunks(npixels) * (atr::kMaskChunk / 64); }

@@ -273,6 +273,7 @@ def scatter_bgr_host(packed, dst_index, image) -> None:
 
 
 MASK_CHUNK = 8192  # pixels per chunk of the masked stream (exchange.hip)
+MASK_MAGIC = 0x4E525441  # "ATRN": the masked stream layout with group offsets (exchange.hip)
 
 
 def background_value(fb) -> int:
@@ -284,7 +285,7 @@ def background_value(fb) -> int:
 
 def pack_bgr_masked_host(fb, background: int) -> np.ndarray:
     """Host reference of atr_pack_bgr_masked: the same bytes as the device stream (header, chunk
-    offsets, mask words, B, G, R of every pixel != background)."""
+    offsets, mask words, group offsets, B, G, R of every pixel != background)."""
     fb = np.ascontiguousarray(np.asarray(fb, np.uint32))
     n = fb.size
     nc = -(-n // MASK_CHUNK)
@@ -293,17 +294,19 @@ def pack_bgr_masked_host(fb, background: int) -> np.ndarray:
     words = np.packbits(nb.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel().astype("<u4")
     counts = nb.reshape(nc, MASK_CHUNK).sum(1) if nc else np.zeros(0, np.int64)
     off = (np.cumsum(counts) - counts).astype("<u4")
+    gcounts = nb.reshape(-1, 64).sum(1)  # every 64-pixel group's payload pixels
+    goff = (np.cumsum(gcounts) - gcounts).astype("<u4")
     total = int(counts.sum())
-    hdr = np.array([0x4D525441, int(background) & 0xFFFFFFFF, nc, total], "<u4")
+    hdr = np.array([MASK_MAGIC, int(background) & 0xFFFFFFFF, nc, total], "<u4")
     pay = pack_bgr_host(fb[nb[:n]]) if total else np.zeros(0, np.uint8)
-    return np.concatenate([hdr.view(np.uint8), off.view(np.uint8), words.view(np.uint8), pay])
+    return np.concatenate([hdr.view(np.uint8), off.view(np.uint8), words.view(np.uint8), goff.view(np.uint8), pay])
 
 
 def scatter_bgr_masked_host(stream, npixels: int, dst_index, image) -> None:
     """Host reference of atr_scatter_bgr_masked: image[dst_index[i]] = pixel i of the stream."""
     b = np.asarray(stream, np.uint8)
     hdr = b[:16].view("<u4")
-    assert int(hdr[0]) == 0x4D525441, "not a masked exchange stream"
+    assert int(hdr[0]) == MASK_MAGIC, "not a masked exchange stream"
     bg, nc, total = int(hdr[1]), int(hdr[2]), int(hdr[3])
     assert nc == -(-npixels // MASK_CHUNK)
     w0 = 16 + 4 * nc
@@ -311,7 +314,8 @@ def scatter_bgr_masked_host(stream, npixels: int, dst_index, image) -> None:
     bits = np.unpackbits(words.astype(">u4").view(np.uint8).reshape(-1, 4), axis=1)
     nb = bits.reshape(-1, 32)[:, ::-1].ravel()[:npixels].astype(bool)
     vals = np.full(npixels, bg, np.uint32)
-    p = b[w0 + 4 * nc * (MASK_CHUNK // 32):][:3 * total].reshape(-1, 3).astype(np.uint32)
+    p0 = w0 + 4 * nc * (MASK_CHUNK // 32) + 4 * nc * (MASK_CHUNK // 64)  # past the masks and group offsets
+    p = b[p0:][:3 * total].reshape(-1, 3).astype(np.uint32)
     vals[nb] = p[:, 0] | (p[:, 1] << 8) | (p[:, 2] << 16)
     image[np.asarray(dst_index, np.int64)] = vals
 

@@ -324,9 +324,10 @@ int atr_scatter_bgr(atr_ctx* ctx, const uint8_t* packed, int64_t npixels, const 
 /* Lossless masked exchange (round 6): frames that are mostly one background value (a c3 frame is
    86% sky) travel as a bit per pixel plus 3 bytes for each pixel that differs from `background`
    (any value is correct; the common one compresses best): ~0.54 B per c3 pixel instead of 3.
-   Stream: a 16-byte header {magic "ATRM", background, chunks, payload pixels}, one u32 payload
-   offset per 8192-pixel chunk, 1 KB of mask bits per chunk, then B, G, R of every non-background
-   pixel in order. atr_pack_bgr_masked_bound(n) = the largest stream for n pixels (host, no device;
+   Stream: a 16-byte header {magic "ATRN", background, chunks, payload pixels}, one u32 payload
+   offset per 8192-pixel chunk, 1 KB of mask bits per chunk, 512 B of group offsets per chunk (the
+   payload offset of every 64 pixels, so decoders need no scan), then B, G, R of every
+   non-background pixel in order. atr_pack_bgr_masked_bound(n) = the largest stream for n pixels (host, no device;
    size `out` by it); atr_pack_bgr_masked writes the stream and its exact byte count to the DEVICE
    int64 *nbytes (the sender ships that many bytes); atr_scatter_bgr_masked decodes a stream of
    npixels into image[dst_index[i]] (as atr_scatter_bgr). Device pointers; async on `stream`;

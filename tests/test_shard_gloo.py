@@ -188,7 +188,8 @@ def test_assembly_share():
 def test_masked_exchange_host_roundtrip():
     """The masked exchange's host references (atr_pack_bgr_masked / atr_scatter_bgr_masked): any
     background value, ragged chunk counts and empty input round-trip exactly, and the stream length
-    is header + chunk offsets + 1 KB of mask per 8192-pixel chunk + 3 B per non-background pixel."""
+    is header + chunk offsets + 1 KB of mask and 512 B of group offsets per 8192-pixel chunk + 3 B
+    per non-background pixel."""
     from atray_amd.shard import pack_bgr_masked_host, scatter_bgr_masked_host, background_value
     rng = np.random.default_rng(7)
     for n in (0, 1, 63, 64, 65, 8191, 8192, 8193, 70001):
@@ -197,7 +198,7 @@ def test_masked_exchange_host_roundtrip():
         for b in (bg, background_value(fb), 0x01000000):
             st = pack_bgr_masked_host(fb, b)
             nc = -(-n // 8192)
-            assert st.size == 16 + 4 * nc + 1024 * nc + 3 * int((fb != b).sum())
+            assert st.size == 16 + 4 * nc + 1024 * nc + 512 * nc + 3 * int((fb != b).sum())
             perm = rng.permutation(n)
             img = np.zeros(n, np.uint32)
             scatter_bgr_masked_host(st, n, perm, img)
