@@ -185,6 +185,27 @@ def test_assembly_share():
     assert assembly_share(n, 1e-6, 8) == 0.5  # capped
 
 
+def test_masked_stream_group_offsets():
+    """The stream's group offsets (layout "ATRN", exchange.hip): word k of chunk c is the payload
+    pixel index of pixel 64 k of the chunk -- the count of non-background pixels before it in the
+    whole stream -- so a decoder reads a 64-pixel group's payload without a scan."""
+    from atray_amd.shard import MASK_CHUNK, MASK_MAGIC, pack_bgr_masked_host
+    rng = np.random.default_rng(11)
+    for n in (1, 64, 8191, 8192, 20000):
+        bg = 0x00123456
+        fb = np.where(rng.random(n) < 0.3, rng.integers(0, 1 << 24, n), bg).astype(np.uint32)
+        st = pack_bgr_masked_host(fb, bg)
+        hdr = st[:16].view("<u4")
+        nc = int(hdr[2])
+        assert int(hdr[0]) == MASK_MAGIC and nc == -(-n // MASK_CHUNK)
+        g0 = 16 + 4 * nc + 4 * nc * (MASK_CHUNK // 32)
+        goff = st[g0:g0 + 4 * nc * (MASK_CHUNK // 64)].view("<u4")
+        nb = np.zeros(nc * MASK_CHUNK, bool)
+        nb[:n] = fb != bg
+        want = np.concatenate([[0], np.cumsum(nb)])[::64][:nc * (MASK_CHUNK // 64)]
+        assert np.array_equal(goff, want)
+
+
 def test_masked_exchange_host_roundtrip():
     """The masked exchange's host references (atr_pack_bgr_masked / atr_scatter_bgr_masked): any
     background value, ragged chunk counts and empty input round-trip exactly, and the stream length
