@@ -348,8 +348,8 @@ int atr_unpack_masked(atr_ctx* ctx, const atr_tile* tiles, int32_t ntiles, int32
    rendered with), its stream at packed[i] (device), nframes frames each, image_stride apart; with
    raw[i] nonzero (raw may be NULL) packed[i] is that render's u32 PACKED framebuffer itself (rank
    0's own frames), copied in by the same launch. The same pixels as atr_unpack_masked (or
-   atr_unpack) per source, from one group-offset and one decode launch per 16 sources instead of two
-   launches, an allocation and an event per source. Asynchronous on `stream`. */
+   atr_unpack) per source, from one decode launch per 16 sources instead of a launch and an event
+   per source. Asynchronous on `stream`. */
 int atr_unpack_masked_ranks(atr_ctx* ctx, int32_t nsrc, const atr_tile* const* tiles, const int32_t* ntiles,
                             int32_t width, int32_t height, const uint8_t* const* packed, const int32_t* raw,
                             int32_t nframes, uint32_t* image, int64_t image_stride, void* stream);
